@@ -1,0 +1,36 @@
+# Build: the HIP product library (gfx950), the CPU oracle (test infrastructure)
+# and the C++ host-mirror check program.  `make -j` is safe.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := qkd_ldpc_v_amd
+CSRC := $(PKG)/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result
+LIB := $(PKG)/libqkdldpc_hip.so
+ORACLE := oracle/libqkdldpc_oracle.so
+HOSTCHK := $(PKG)/host/host_mirror_check
+
+all: $(LIB) $(ORACLE) $(HOSTCHK)
+
+$(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/loaders.o: $(CSRC)/loaders.cpp $(CSRC)/loaders.hpp
+	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
+
+$(LIB): $(CSRC)/decoder.o $(CSRC)/capi.o $(CSRC)/loaders.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
+
+$(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h
+	$(MAKE) -C oracle
+
+$(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)
+	g++ -O2 -std=c++17 -Wall -I include $< -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/..' -o $@
+
+clean:
+	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK)
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean

@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Decoded info-bits/s of the QKD-LDPC decode hot path on MI355X.
+
+A step = the reference's per-trial window (QKD_LDPC, src/qkd_ldpc_algorithm.cpp:
+1031-1087; timed like src/simulation.cpp:559-568) for one batch of frames:
+LLR build + Alice syndrome on device, the BP decode, the key comparison.  The
+trials (synthetic BSC keys) are generated before timing and are resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c1|c4]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Frames are sharded across ranks with no data-path collective (weak scaling:
+every GPU decodes its own batch); a barrier + max-over-ranks bracket the timed
+region.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "decoded info-bits/sec (whole node), n=10k R=0.8 SPA 50-iter, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+WORKLOADS = {
+    # name: matrix fixture, format, algorithm, primary, secondary, qber, batch/GPU, description
+    "c2": ("c2_n10240_m2201.alist", 1, 0, 0.0, 0.0, 0.0215, 4096,
+           "C2: n=10k R=0.8 SPA 50-iter, batch 4096/GPU (configs_all/config 10k SPA FER=0.01.json bucket 0.795)"),
+    "c3": ("c3_n10240_m1801.alist", 1, 3, 0.77, 0.0, 0.015, 4096,
+           "C3: n=10k R=0.82 OMSA beta=0.77 50-iter, batch 4096/GPU"),
+    "c1": ("c1_n1024_m220.alist", 1, 0, 0.0, 0.0, 0.013, 4096, "C1: n=1k R~0.8 SPA 50-iter"),
+    "c4": ("c4s_n102400_m32001.alist", 1, 0, 0.0, 0.0, 0.038, 128,
+           "C4 stand-in: n=100k R=0.69 SPA 50-iter, batch 128/GPU (R=0.79 file absent upstream)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="frames per GPU (default: the workload's)")
+    ap.add_argument("--max-iterations", type=int, default=50)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    import qkd_ldpc_v_amd as Q
+
+    fixture, fmt, alg, prim, sec, qber, batch, desc = WORKLOADS[args.workload]
+    batch = args.batch or batch
+    H = Q.load_matrix(os.path.join(ROOT, "tests", "golden", "matrices", fixture + ".gz"), fmt)
+    n, m, E = H.n, H.m, H.nnz
+    k_info = n - m
+    g = Q.Graph(H)
+    plan = g.plan(local, alg)
+    params = Q.Params(alg, args.max_iterations, True, 100.0, prim, sec)
+
+    # ---- trials (not timed): synthetic BSC keys, resident in HBM ----
+    a, b, q_acc = Q.bsc_frames(n, qber, batch, seed=1022025 + 7919 * rank)
+    lp = Q.log_p(q_acc)
+    ta = torch.from_numpy(a).to(dev)
+    tb = torch.from_numpy(b).to(dev)
+    tlp = torch.full((batch,), lp, dtype=torch.float64, device=dev)
+    llr_ws = torch.empty((batch, n), dtype=torch.float64, device=dev)
+    syn_ws = torch.empty((batch, m), dtype=torch.uint8, device=dev)
+    bits = torch.empty((batch, n), dtype=torch.uint8, device=dev)
+    iters = torch.empty(batch, dtype=torch.int32, device=dev)
+    ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+    km = torch.empty(batch, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        g.build_frames_device(ta, tb, tlp, llr_ws, syn_ws, stream=stream)
+        if i is not None:
+            ev0[i].record(stream)
+        g.decode_device(params, llr_ws, syn_ws, bits, iters, ok, stream=stream)
+        if i is not None:
+            ev1[i].record(stream)
+        Q.keys_match_device(ta, bits, km, stream=stream)
+
+    log(f"[rank {rank}] {desc}; plan {plan}; warmup {args.warmup}")
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([ev0[i].elapsed_time(ev1[i]) for i in range(args.steps)]))
+
+    it_sum = int(iters.to(torch.int64).sum().item())
+    n_ok = int(ok.to(torch.int64).sum().item())
+    n_keys = int(km.to(torch.int64).sum().item())
+    stats = torch.tensor([elapsed, it_sum, n_ok, n_keys, batch, kernel_ms], dtype=torch.float64, device=dev)
+    if dist:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        elapsed_max, kernel_ms_max = float(mx[0]), float(mx[5])
+    else:
+        elapsed_max, kernel_ms_max = elapsed, kernel_ms
+    it_total, ok_total, keys_total, frames_step = (float(stats[1]), float(stats[2]), float(stats[3]), float(stats[4]))
+
+    if rank == 0:
+        frames_total = frames_step * args.steps
+        value = frames_total * k_info / elapsed_max
+        B = 8.0 * (2 * E + 2 * n)  # algorithmic bytes per frame-iteration
+        # per-launch algorithmic bytes of THIS rank's decode kernel / its mean duration
+        achieved = (it_sum * B) / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "info-bits/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic BSC sifted keys (exactly floor(n*QBER) flips per frame, numpy PCG64), "
+                    "reference parity-check matrix file",
+            "config": {
+                "workload": desc, "matrix": fixture, "n": n, "m": m, "edges": E, "info_bits_per_frame": k_info,
+                "algorithm": Q.ALGORITHM_NAMES[alg], "qber": qber, "max_iterations": args.max_iterations,
+                "batch_per_gpu": batch, "global_batch": int(frames_step),
+                "parallelism": f"frames sharded over {world} GPU(s), no collectives",
+                "kernel_variant": plan["variant"], "lanes_per_frame": plan["lanes"],
+                "edges_per_lane": plan["edges_per_lane"], "workgroups": plan["workgroups"],
+            },
+            "fer": 1.0 - ok_total / frames_step,
+            "key_mismatch_rate": 1.0 - keys_total / frames_step,
+            "mean_iterations": it_total / frames_step,
+            "decode_kernel_ms": kernel_ms,
+            "decode_kernel_ms_max_rank": kernel_ms_max,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "bytes_per_frame_iteration": B,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
+                                               args.cpu_baseline_seconds, k_info)
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info):
+    """The CPU oracle (a port of the reference decoder, glibc math, one frame per
+    task on a thread pool like src/simulation.cpp:721,740-746) on a bounded
+    sample of the same workload: chunks of frames until `seconds` elapse."""
+    import qkd_ldpc_v_amd as Q
+    from oracle.pyoracle import Oracle
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    O = Oracle(H)
+    p = O.params(alg, max_it, True, 100.0, prim, sec)
+    chunk = threads * 4
+    frames = 0
+    t_dec = 0.0
+    seed = 5
+    while t_dec < seconds:
+        a, b, q = Q.bsc_frames(H.n, qber, chunk, seed=seed)
+        seed += 1
+        t0 = time.perf_counter()
+        lp = math.log((1.0 - q) / q)
+        llr = np.where(b != 0, -lp, lp)
+        s = H.syndrome(a)
+        bits, it, ok, _ = O.decode_batch(p, llr, s, threads=threads)
+        (bits == a).all(axis=1)
+        t_dec += time.perf_counter() - t0
+        frames += chunk
+    return {"value": frames * k_info / t_dec, "unit": "info-bits/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} frames of the same workload (chunks of {chunk}), {t_dec:.1f} s, "
+                      f"oracle/ldpc_oracle.c on {threads} host threads"}
+
+
+if __name__ == "__main__":
+    main()

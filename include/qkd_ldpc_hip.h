@@ -1,0 +1,176 @@
+/* qkd_ldpc_hip.h — C ABI of libqkdldpc_hip.so, the MI355X (gfx950) LDPC
+ * belief-propagation decoder for QKD error reconciliation.
+ *
+ * This is the drop-in boundary for the hot path of ColdCloudd/QKD_LDPC_V:
+ * the six flooding decoders of src/qkd_ldpc_algorithm.cpp:3-1029 (declared at
+ * src/qkd_ldpc_algorithm.hpp:28-90), batched over independent trials — the
+ * pool.detach_loop seam at src/simulation.cpp:740-746 — plus the per-trial frame
+ * construction of QKD_LDPC (src/qkd_ldpc_algorithm.cpp:1031-1087) and the H
+ * loaders it reads (src/array_and_matrix_operations.cpp:291-886).
+ *
+ * Plain C: pointers and sizes only.  Every entry returns 0 on success and a
+ * negative QLDPC_E* code on failure; qldpc_last_error() then describes it
+ * (thread-local).  The C++ mirror in qkd_ldpc_v_amd/host/qkd_ldpc_algorithm.hpp
+ * turns failures into std::runtime_error, as the reference's loaders do.
+ */
+#ifndef QKD_LDPC_HIP_H
+#define QKD_LDPC_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QLDPC_OK 0
+#define QLDPC_EINVAL (-1)   /* bad argument / malformed graph */
+#define QLDPC_EHIP (-2)     /* HIP runtime failure */
+#define QLDPC_EIO (-3)      /* matrix file cannot be opened / parsed */
+#define QLDPC_ENOMEM (-4)
+#define QLDPC_EUNSUP (-5)   /* graph shape the GPU path does not accept */
+
+/* Decoder ids: reference src/config.hpp:201 (DEC_SPA=0 ... DEC_AOMSA=5). */
+#define QLDPC_SPA 0
+#define QLDPC_SPA_LIN 1
+#define QLDPC_NMSA 2
+#define QLDPC_OMSA 3
+#define QLDPC_ANMSA 4
+#define QLDPC_AOMSA 5
+
+/* Matrix file formats: reference src/config.hpp:202 (MAT_*). */
+#define QLDPC_MAT_UNCOMPRESSED 0
+#define QLDPC_MAT_ALIST 1
+#define QLDPC_MAT_SPARSE_1 2
+#define QLDPC_MAT_SPARSE_2 3
+
+typedef struct qldpc_graph qldpc_graph;
+
+/* Decoder parameters.  Replaces the per-call arguments of the six decoders
+ * (src/qkd_ldpc_algorithm.hpp:28-90) plus the global-CFG inputs they read:
+ * CFG.DECODING_ALGORITHM (dispatch at src/qkd_ldpc_algorithm.cpp:1056-1085),
+ * CFG.DECODING_ALG_MAX_ITERATIONS, CFG.ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD and
+ * CFG.DECODING_ALG_MSG_LLR_THRESHOLD; primary/secondary are
+ * decoding_scaling_factors (src/config.hpp:50-54). */
+typedef struct {
+    int32_t algorithm;      /* QLDPC_SPA .. QLDPC_AOMSA */
+    int32_t max_iterations; /* >= 1 */
+    int32_t thr_enabled;    /* message LLR clipping on/off */
+    int32_t reserved;
+    double thr;             /* clipping threshold (> 0 when enabled) */
+    double primary;         /* alpha (NMSA, ANMSA) or beta (OMSA, AOMSA) */
+    double secondary;       /* nu (ANMSA) or sigma (AOMSA) */
+} qldpc_params;
+
+/* ---------------------------------------------------------------- loaders */
+
+/* Parse a parity-check matrix file into the reference's H_matrix adjacency
+ * (check_nodes -> row_ptr/col_idx, bit_nodes -> col_ptr/row_idx).  Restates
+ * read_sparse_uncompressed_matrix / read_sparse_matrix_alist /
+ * read_sparse_matrix_1 / read_sparse_matrix_2
+ * (src/array_and_matrix_operations.cpp:764-886, 291-468, 478-617, 626-761),
+ * including their validation errors.  Files ending in ".gz" are inflated first.
+ * Call with NULL arrays to query n, m and nnz; then again with buffers of
+ * m+1, nnz, n+1 and nnz entries.  *is_regular mirrors H_matrix::is_regular. */
+int qldpc_load_matrix(const char *path, int32_t format, int32_t *n, int32_t *m, int32_t *nnz,
+                      int32_t *row_ptr, int32_t *col_idx, int32_t *col_ptr, int32_t *row_idx,
+                      int32_t *is_regular);
+
+/* ------------------------------------------------------------------ graph */
+
+/* Build the device-resident Tanner graph from check_nodes in CSR form
+ * (row_ptr[m+1], col_idx[nnz]; bit ids of row j in ascending order).  The graph
+ * is immutable, replicated on every device of device_mask (bit d = HIP device
+ * d; 0 = current device only) and safe to share between host threads. */
+int qldpc_graph_create(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                       int32_t device_mask, qldpc_graph **out);
+
+/* As qldpc_graph_create, additionally checking that bit_nodes
+ * (col_ptr[n+1], row_idx[nnz]) is the ascending transpose of check_nodes — the
+ * pairing the reference's slot counters assume (src/qkd_ldpc_algorithm.cpp:
+ * 67-69,116-118).  Unsorted or inconsistent lists return QLDPC_EUNSUP. */
+int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr,
+                               const int32_t *col_idx, const int32_t *col_ptr,
+                               const int32_t *row_idx, int32_t device_mask, qldpc_graph **out);
+
+void qldpc_graph_destroy(qldpc_graph *g);
+
+/* n, m, nnz and the number of devices the graph lives on. */
+int qldpc_graph_info(const qldpc_graph *g, int32_t *n, int32_t *m, int32_t *nnz,
+                     int32_t *num_devices);
+
+/* ----------------------------------------------------------------- decode */
+
+/* Decode `batch` independent frames held in HOST memory; synchronous.
+ * Replaces `batch` calls of the decoder selected by p->algorithm, each
+ *   decoding_result f(llr, H, syndrome, max_it, [alpha|beta], [nu|sigma], thr, out)
+ * (src/qkd_ldpc_algorithm.hpp:28-90).  llr: batch*n doubles (frame-major),
+ * syndrome: batch*m bytes in {0,1}, bits_out: batch*n bytes (bit_array_out),
+ * iters_out / synd_ok_out: decoding_result {iterations_num, syndromes_match}
+ * per frame, posterior_out (nullable): batch*n doubles = the reference's
+ * total_bit_llr at return.  Frames are split in contiguous slices over the
+ * graph's devices, one host thread per device, no collectives. */
+int qldpc_decode_batch(qldpc_graph *g, const qldpc_params *p, int32_t batch, const double *llr,
+                       const uint8_t *syndrome, uint8_t *bits_out, uint32_t *iters_out,
+                       uint8_t *synd_ok_out, double *posterior_out);
+
+/* Same on DEVICE buffers of the graph's device `device`, enqueued on the HIP
+ * stream `stream` (hipStream_t; NULL = default stream).  Asynchronous. */
+int qldpc_decode_batch_device(qldpc_graph *g, int32_t device, const qldpc_params *p, int32_t batch,
+                              const double *d_llr, const uint8_t *d_syndrome, uint8_t *d_bits_out,
+                              uint32_t *d_iters_out, uint8_t *d_synd_ok_out,
+                              double *d_posterior_out, void *stream);
+
+/* ------------------------------------------------ per-trial frame (QKD_LDPC) */
+
+/* QKD_LDPC's frame construction on device (src/qkd_ldpc_algorithm.cpp:
+ * 1043-1052): llr[i] = bob[i] ? -log_p : log_p, syndrome = H * alice
+ * (calculate_syndrome, src/array_and_matrix_operations.cpp:936-950).
+ * d_alice/d_bob: batch*n bytes in {0,1}.  d_log_p: batch doubles, each
+ * log((1-q)/q) of the trial's accurate QBER q evaluated by the HOST C library
+ * (qldpc_log_p below): glibc's log is not correctly rounded, so evaluating it
+ * anywhere else could move an LLR by an ulp. */
+int qldpc_build_frames_device(qldpc_graph *g, int32_t device, int32_t batch, const uint8_t *d_alice,
+                              const uint8_t *d_bob, const double *d_log_p, double *d_llr,
+                              uint8_t *d_syndrome, void *stream);
+
+/* log((1. - q) / q) with the host C library, as src/qkd_ldpc_algorithm.cpp:1043. */
+double qldpc_log_p(double qber);
+
+/* keys_match = arrays_equal(alice, bob_solution) per frame
+ * (src/qkd_ldpc_algorithm.cpp:1087; src/array_and_matrix_operations.cpp:105-118). */
+int qldpc_keys_match_device(int32_t batch, int32_t n, const uint8_t *d_alice,
+                            const uint8_t *d_bits, uint8_t *d_keys_match, void *stream);
+
+/* The whole per-trial window of QKD_LDPC for `batch` trials on device: frame
+ * construction + decode + key comparison.  d_llr_ws / d_synd_ws: caller-owned
+ * workspaces of batch*n doubles and batch*m bytes. */
+int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_params *p,
+                                int32_t batch, const uint8_t *d_alice, const uint8_t *d_bob,
+                                const double *d_log_p, double *d_llr_ws, uint8_t *d_synd_ws,
+                                uint8_t *d_bits_out, uint32_t *d_iters_out,
+                                uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out, void *stream);
+
+/* --------------------------------------------------------------- introspection */
+
+/* Launch geometry the decoder uses for this graph on `device`: lanes per frame
+ * (threads per workgroup), edges per lane, resident workgroups, dynamic LDS
+ * bytes and the kernel variant name (static string). */
+int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, int32_t *lanes,
+                     int32_t *edges_per_lane, int32_t *workgroups, int32_t *lds_bytes,
+                     const char **variant);
+
+/* Diagnostic: evaluate the decoder's device math on `count` inputs on the
+ * current device — fn 0 tanh, 1 atanh, 2 expm1, 3 log1p (exact_math.h, the
+ * glibc-exact restatement used by the SPA kernel), 4 tanh_lin_approx,
+ * 5 atanh_lin_approx (src/qkd_ldpc_algorithm.cpp:146-172). */
+int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream);
+
+/* Thread-local description of the last failure on this thread. */
+const char *qldpc_last_error(void);
+
+/* Library version string. */
+const char *qldpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,16 @@
+"""qkd_ldpc_v_amd — MI355X (gfx950) LDPC belief-propagation decoding for QKD.
+
+The product is libqkdldpc_hip.so (HIP kernels + C ABI, include/qkd_ldpc_hip.h);
+this package binds it and mirrors the reference's decode interface
+(ColdCloudd/QKD_LDPC_V src/qkd_ldpc_algorithm.hpp).
+"""
+from ._lib import (ALGORITHM_NAMES, ANMSA, AOMSA, NMSA, OMSA, SPA, SPA_LIN, Params, QLDPCError, exported_symbols, lib,
+                   log_p, version)
+from .graph import DecodeOutput, Graph, HMatrix, keys_match_device, load_matrix
+from .trials import bsc_frames
+
+__all__ = [
+    "ALGORITHM_NAMES", "ANMSA", "AOMSA", "NMSA", "OMSA", "SPA", "SPA_LIN", "Params", "QLDPCError",
+    "exported_symbols", "lib", "log_p", "version", "DecodeOutput", "Graph", "HMatrix", "keys_match_device",
+    "load_matrix", "bsc_frames",
+]

@@ -1,0 +1,593 @@
+// capi.hip — the C ABI of libqkdldpc_hip.so (include/qkd_ldpc_hip.h).
+//
+// Graph planning: the Tanner graph of H (the reference's H_matrix,
+// src/array_and_matrix_operations.hpp:60-77) is turned once into the decoder's
+// lane partition — E edges in CSR order dealt EPL-per-lane to T lanes — plus a
+// row-ELL copy for syndrome checks, and replicated on each device of the
+// graph.  Decoding is the persistent kernel of decoder.hip; the host-buffer
+// entry shards frames over devices (one host thread per device, contiguous
+// slices, no collectives) — the multi-GPU analogue of the reference's
+// BS::thread_pool over trials (src/simulation.cpp:721,740-746).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/qkd_ldpc_hip.h"
+#include "decoder.hpp"
+#include "loaders.hpp"
+
+using namespace qldpc;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char *what) {
+    return fail(QLDPC_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                         \
+    do {                                                      \
+        hipError_t _e = (expr);                               \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);     \
+    } while (0)
+
+constexpr size_t LDS_LIMIT = 160 * 1024;
+
+struct Workspace {  // per (device, stream): frame counter + decoder scratch
+    int *counter = nullptr;
+    double *scratch = nullptr;
+    size_t scratch_doubles = 0;
+};
+
+struct HostIO {  // device staging buffers of the host-buffer entry
+    double *llr = nullptr, *post = nullptr;
+    uint8_t *synd = nullptr, *bits = nullptr, *ok = nullptr;
+    uint32_t *iters = nullptr;
+    size_t cap_frames = 0;
+    hipStream_t stream = nullptr;
+};
+
+struct DeviceGraph {
+    int device = 0;
+    int num_cus = 0;
+    uint32_t *slot_meta = nullptr;
+    int32_t *lane_row0 = nullptr, *lane_head = nullptr, *ell_col = nullptr, *row_deg = nullptr;
+    std::mutex mu;
+    std::map<void *, Workspace> ws;
+    HostIO io;
+    int occ[6] = {0, 0, 0, 0, 0, 0};
+};
+
+}  // namespace
+
+struct qldpc_graph {
+    int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
+    std::vector<std::unique_ptr<DeviceGraph>> devs;
+};
+
+namespace {
+
+const char *variant_name(int v) {
+    switch (v) {
+    case VAR_REG_LDS: return "reg_lds";
+    case VAR_GLB_LDS: return "glb_lds";
+    default: return "glb_glb";
+    }
+}
+
+int round_up64(long long x) { return (int)(((x + 63) / 64) * 64); }
+
+// Choose (variant, T, EPL).  max_dc <= EPL keeps any row within two lanes.
+void plan(qldpc_graph &g) {
+    const long long E = g.E;
+    // Register-resident messages: EPL_REG edges per lane at most.
+    {
+        int T = std::max(64, round_up64((E + EPL_REG - 1) / EPL_REG));
+        if (T <= 1024) {
+            int EPL = (int)((E + T - 1) / T);
+            if (EPL < 1) EPL = 1;
+            while (g.max_dc > EPL && T > 64) {
+                T -= 64;
+                EPL = (int)((E + T - 1) / T);
+            }
+            if (g.max_dc <= EPL && EPL <= EPL_REG && lds_bytes_for(VAR_REG_LDS, g.n, g.m, T) <= LDS_LIMIT) {
+                g.variant = VAR_REG_LDS;
+                g.T = T;
+                g.EPL = EPL;
+                return;
+            }
+        }
+    }
+    // Messages in global scratch: as many lanes as the workgroup allows.
+    int T = (int)std::min<long long>(1024, std::max(64, round_up64((E + 7) / 8)));
+    int EPL = (int)((E + T - 1) / T);
+    while (g.max_dc > EPL && T > 64) {
+        T -= 64;
+        EPL = (int)((E + T - 1) / T);
+    }
+    g.T = T;
+    g.EPL = std::max(EPL, 1);
+    g.variant = (lds_bytes_for(VAR_GLB_LDS, g.n, g.m, T) <= LDS_LIMIT) ? VAR_GLB_LDS : VAR_GLB_GLB;
+}
+
+template <typename T>
+int upload(T **dst, const std::vector<T> &src) {
+    const size_t bytes = std::max<size_t>(1, src.size()) * sizeof(T);
+    HIP_TRY(hipMalloc(dst, bytes));
+    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return QLDPC_OK;
+}
+
+int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx, int32_t device_mask,
+                qldpc_graph **out) {
+    if (!out) return fail(QLDPC_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n <= 0 || m < 0 || !row_ptr || (!col_idx && row_ptr[m] > 0))
+        return fail(QLDPC_EINVAL, "invalid graph dimensions or NULL arrays");
+    if (n > MAX_N) return fail(QLDPC_EUNSUP, "n exceeds 2^20 bit nodes");
+    if (row_ptr[0] != 0) return fail(QLDPC_EINVAL, "row_ptr[0] must be 0");
+    for (int j = 0; j < m; ++j)
+        if (row_ptr[j + 1] < row_ptr[j]) return fail(QLDPC_EINVAL, "row_ptr must be non-decreasing");
+    const int E = row_ptr[m];
+    if (E <= 0) return fail(QLDPC_EINVAL, "graph has no edges");
+
+    auto g = std::make_unique<qldpc_graph>();
+    g->n = n;
+    g->m = m;
+    g->E = E;
+    std::vector<int> dv(n, 0);
+    for (int j = 0; j < m; ++j) {
+        g->max_dc = std::max(g->max_dc, row_ptr[j + 1] - row_ptr[j]);
+        for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
+            const int c = col_idx[e];
+            if (c < 0 || c >= n) return fail(QLDPC_EINVAL, "col_idx entry out of range [0, n)");
+            if (e > row_ptr[j] && col_idx[e - 1] >= c)
+                return fail(QLDPC_EUNSUP, "check_nodes rows must list bit ids in strictly ascending order");
+            ++dv[c];
+        }
+    }
+    for (int i = 0; i < n; ++i) g->dv_max = std::max(g->dv_max, dv[i]);
+    if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 64");
+    plan(*g);
+    const int T = g->T, EPL = g->EPL;
+
+    // Lane partition metadata.
+    std::vector<int> row_of(E), kpos(E), seen(n, 0);
+    for (int j = 0; j < m; ++j)
+        for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
+            row_of[e] = j;
+            kpos[e] = seen[col_idx[e]]++;
+        }
+    // uint4 groups per lane, group-major [g][lane][4]; the register variant
+    // always has EPL_REG/4 groups at lane stride REG_TSTRIDE.
+    const bool reg = g->variant == VAR_REG_LDS;
+    const int G4 = reg ? EPL_REG / 4 : (EPL + 3) / 4;
+    const int TS = reg ? REG_TSTRIDE : T;
+    std::vector<uint32_t> meta((size_t)G4 * TS * 4, 0);
+    std::vector<int32_t> lrow0(T, -1), lhead(T, 0);
+    for (int l = 0; l < T; ++l) {
+        const long long e0 = (long long)l * EPL;
+        if (e0 < E) {
+            const int r0 = row_of[e0];
+            lrow0[l] = r0;
+            if (e0 != row_ptr[r0]) lhead[l] = row_ptr[r0 + 1] - (int)e0;
+        }
+        int prev_row = -1;
+        for (int k = 0; k < EPL; ++k) {
+            const long long e = e0 + k;
+            if (e >= E) break;
+            const int j = row_of[e];
+            uint32_t w = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
+            if (e == row_ptr[j]) w |= META_START;
+            if (e == row_ptr[j + 1] - 1) w |= META_END;
+            if (k > 0 && j != prev_row && j != prev_row + 1)
+                return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
+            prev_row = j;
+            meta[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = w;
+        }
+    }
+    // Row-ELL (slot-major) for syndrome evaluation.
+    const int dcm = std::max(1, g->max_dc);
+    std::vector<int32_t> ell((size_t)dcm * std::max(m, 1), 0), rdeg(std::max(m, 1), 0);
+    for (int j = 0; j < m; ++j) {
+        rdeg[j] = row_ptr[j + 1] - row_ptr[j];
+        for (int k = 0; k < rdeg[j]; ++k) ell[(size_t)k * m + j] = col_idx[row_ptr[j] + k];
+    }
+
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    std::vector<int> devices;
+    if (device_mask == 0) {
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        devices.push_back(cur);
+    } else {
+        for (int d = 0; d < 31; ++d)
+            if (device_mask & (1 << d)) {
+                if (d >= ndev) return fail(QLDPC_EINVAL, "device_mask names a device that does not exist");
+                devices.push_back(d);
+            }
+    }
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    for (int d : devices) {
+        auto dg = std::make_unique<DeviceGraph>();
+        dg->device = d;
+        HIP_TRY(hipSetDevice(d));
+        HIP_TRY(hipDeviceGetAttribute(&dg->num_cus, hipDeviceAttributeMultiprocessorCount, d));
+        int rc;
+        if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->lane_row0, lrow0)) ||
+            (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->ell_col, ell)) ||
+            (rc = upload(&dg->row_deg, rdeg))) {
+            (void)hipSetDevice(prev);
+            return rc;
+        }
+        g->devs.push_back(std::move(dg));
+    }
+    HIP_TRY(hipSetDevice(prev));
+    *out = g.release();
+    return QLDPC_OK;
+}
+
+DeviceGraph *find_dev(qldpc_graph *g, int device) {
+    for (auto &d : g->devs)
+        if (d->device == device) return d.get();
+    return nullptr;
+}
+
+int check_params(const qldpc_params *p) {
+    if (!p) return fail(QLDPC_EINVAL, "params is NULL");
+    if (p->algorithm < 0 || p->algorithm > 5) return fail(QLDPC_EINVAL, "algorithm must be 0..5");
+    if (p->max_iterations < 1) return fail(QLDPC_EINVAL, "max_iterations must be >= 1");
+    if (p->thr_enabled && !(p->thr > 0.)) return fail(QLDPC_EINVAL, "threshold must be > 0 when enabled");
+    return QLDPC_OK;
+}
+
+// Enqueue the decoder for `batch` device-resident frames on `stream`.
+int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch, const double *llr,
+              const uint8_t *synd, uint8_t *bits, uint32_t *iters, uint8_t *ok, double *post,
+              hipStream_t stream) {
+    if (batch == 0) return QLDPC_OK;
+    const int alg = p->algorithm;
+    const size_t lds = lds_bytes_for(g->variant, g->n, g->m, g->T);
+    Workspace *w;
+    int wgs;
+    {
+        std::lock_guard<std::mutex> lk(dg->mu);
+        if (dg->occ[alg] == 0) {
+            int b = 0;
+            HIP_TRY(occupancy(g->variant, alg, g->T, lds, &b));
+            if (b <= 0) return fail(QLDPC_EUNSUP, "decoder kernel cannot be resident with this graph shape");
+            dg->occ[alg] = b;
+        }
+        wgs = std::min(batch, dg->occ[alg] * dg->num_cus);
+        w = &dg->ws[(void *)stream];
+        if (!w->counter) HIP_TRY(hipMalloc(&w->counter, 64));
+        const long long per = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+        const size_t need = (size_t)per * (size_t)wgs;
+        if (need > w->scratch_doubles) {
+            if (w->scratch) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                HIP_TRY(hipFree(w->scratch));
+                w->scratch = nullptr;
+            }
+            HIP_TRY(hipMalloc(&w->scratch, need * sizeof(double)));
+            w->scratch_doubles = need;
+        }
+    }
+    DecodeArgs a{};
+    a.n = g->n; a.m = g->m; a.E = g->E; a.T = g->T; a.EPL = g->EPL; a.dv_max = g->dv_max; a.max_dc = g->max_dc;
+    a.slot_meta = dg->slot_meta; a.lane_row0 = dg->lane_row0; a.lane_head = dg->lane_head;
+    a.ell_col = dg->ell_col; a.row_deg = dg->row_deg;
+    a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
+    a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
+    a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
+    a.frame_counter = w->counter;
+    a.scratch = w->scratch;
+    a.scratch_wg_doubles = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
+    HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
+    return QLDPC_OK;
+}
+
+template <typename T>
+int grow(T **p, size_t count) {
+    if (*p) HIP_TRY(hipFree(*p));
+    *p = nullptr;
+    HIP_TRY(hipMalloc(p, std::max<size_t>(count, 1) * sizeof(T)));
+    return QLDPC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *qldpc_last_error(void) { return g_last_error.c_str(); }
+
+const char *qldpc_version(void) { return "qkd_ldpc_v_amd 0.1.0 (gfx950)"; }
+
+double qldpc_log_p(double qber) { return std::log((1. - qber) / qber); }
+
+int qldpc_load_matrix(const char *path, int32_t format, int32_t *n, int32_t *m, int32_t *nnz, int32_t *row_ptr,
+                      int32_t *col_idx, int32_t *col_ptr, int32_t *row_idx, int32_t *is_regular) {
+    if (!path || !n || !m || !nnz) return fail(QLDPC_EINVAL, "path/n/m/nnz must not be NULL");
+    try {
+        const HMatrix H = load_matrix(path, format);
+        long long e_rows = 0, e_cols = 0;
+        for (const auto &r : H.check_nodes) e_rows += (long long)r.size();
+        for (const auto &c : H.bit_nodes) e_cols += (long long)c.size();
+        *n = (int32_t)H.bit_nodes.size();
+        *m = (int32_t)H.check_nodes.size();
+        *nnz = (int32_t)e_rows;
+        if (is_regular) *is_regular = H.is_regular ? 1 : 0;
+        if (e_rows != e_cols)
+            return fail(QLDPC_EINVAL, "check_nodes and bit_nodes hold different edge counts (" +
+                                          std::to_string(e_rows) + " vs " + std::to_string(e_cols) + ")");
+        if (row_ptr && col_idx) {
+            int32_t o = 0;
+            for (size_t j = 0; j < H.check_nodes.size(); ++j) {
+                row_ptr[j] = o;
+                for (int c : H.check_nodes[j]) col_idx[o++] = c;
+            }
+            row_ptr[H.check_nodes.size()] = o;
+        }
+        if (col_ptr && row_idx) {
+            int32_t o = 0;
+            for (size_t i = 0; i < H.bit_nodes.size(); ++i) {
+                col_ptr[i] = o;
+                for (int r : H.bit_nodes[i]) row_idx[o++] = r;
+            }
+            col_ptr[H.bit_nodes.size()] = o;
+        }
+    } catch (const std::exception &e) {
+        return fail(QLDPC_EIO, e.what());
+    }
+    return QLDPC_OK;
+}
+
+int qldpc_graph_create(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx, int32_t device_mask,
+                       qldpc_graph **out) {
+    return build_graph(n, m, row_ptr, col_idx, device_mask, out);
+}
+
+int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                               const int32_t *col_ptr, const int32_t *row_idx, int32_t device_mask,
+                               qldpc_graph **out) {
+    if (!row_ptr || !col_idx || !col_ptr || !row_idx) return fail(QLDPC_EINVAL, "NULL adjacency array");
+    if (n <= 0 || m < 0 || col_ptr[n] != row_ptr[m])
+        return fail(QLDPC_EUNSUP, "bit_nodes and check_nodes hold different edge counts");
+    // bit_nodes must be the ascending transpose of check_nodes.
+    std::vector<int> fill(n, 0);
+    for (int i = 0; i < n; ++i)
+        if (col_ptr[i + 1] < col_ptr[i]) return fail(QLDPC_EINVAL, "col_ptr must be non-decreasing");
+    for (int j = 0; j < m; ++j)
+        for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
+            const int c = col_idx[e];
+            if (c < 0 || c >= n) return fail(QLDPC_EINVAL, "col_idx entry out of range");
+            const int slot = col_ptr[c] + fill[c]++;
+            if (slot >= col_ptr[c + 1] || row_idx[slot] != j)
+                return fail(QLDPC_EUNSUP,
+                            "bit_nodes is not the ascending transpose of check_nodes: the reference's "
+                            "slot pairing would not match edges (unsorted adjacency)");
+        }
+    return build_graph(n, m, row_ptr, col_idx, device_mask, out);
+}
+
+void qldpc_graph_destroy(qldpc_graph *g) {
+    if (!g) return;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    for (auto &d : g->devs) {
+        (void)hipSetDevice(d->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(d->slot_meta);
+        (void)hipFree(d->lane_row0);
+        (void)hipFree(d->lane_head);
+        (void)hipFree(d->ell_col);
+        (void)hipFree(d->row_deg);
+        for (auto &kv : d->ws) {
+            (void)hipFree(kv.second.counter);
+            (void)hipFree(kv.second.scratch);
+        }
+        HostIO &io = d->io;
+        (void)hipFree(io.llr); (void)hipFree(io.post); (void)hipFree(io.synd); (void)hipFree(io.bits); (void)hipFree(io.ok); (void)hipFree(io.iters);
+        if (io.stream) (void)hipStreamDestroy(io.stream);
+    }
+    (void)hipSetDevice(prev);
+    delete g;
+}
+
+int qldpc_graph_info(const qldpc_graph *g, int32_t *n, int32_t *m, int32_t *nnz, int32_t *num_devices) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    if (n) *n = g->n;
+    if (m) *m = g->m;
+    if (nnz) *nnz = g->E;
+    if (num_devices) *num_devices = (int32_t)g->devs.size();
+    return QLDPC_OK;
+}
+
+int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, int32_t *lanes,
+                     int32_t *edges_per_lane, int32_t *workgroups, int32_t *lds_bytes, const char **variant) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    if (algorithm < 0 || algorithm > 5) return fail(QLDPC_EINVAL, "algorithm must be 0..5");
+    DeviceGraph *dg = find_dev(const_cast<qldpc_graph *>(g), device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    const size_t lds = lds_bytes_for(g->variant, g->n, g->m, g->T);
+    if (lanes) *lanes = g->T;
+    if (edges_per_lane) *edges_per_lane = g->EPL;
+    if (lds_bytes) *lds_bytes = (int32_t)lds;
+    if (variant) *variant = variant_name(g->variant);
+    if (workgroups) {
+        int prev = 0;
+        HIP_TRY(hipGetDevice(&prev));
+        HIP_TRY(hipSetDevice(dg->device));
+        int b = 0;
+        hipError_t e = occupancy(g->variant, algorithm, g->T, lds, &b);
+        (void)hipSetDevice(prev);
+        if (e != hipSuccess) return hip_fail(e, "occupancy");
+        *workgroups = b * dg->num_cus;
+    }
+    return QLDPC_OK;
+}
+
+int qldpc_decode_batch_device(qldpc_graph *g, int32_t device, const qldpc_params *p, int32_t batch,
+                              const double *d_llr, const uint8_t *d_syndrome, uint8_t *d_bits_out,
+                              uint32_t *d_iters_out, uint8_t *d_synd_ok_out, double *d_posterior_out,
+                              void *stream) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch > 0 && (!d_llr || !d_syndrome || !d_bits_out || !d_iters_out || !d_synd_ok_out))
+        return fail(QLDPC_EINVAL, "NULL device buffer");
+    DeviceGraph *dg = find_dev(g, device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    rc = decode_on(g, dg, p, batch, d_llr, d_syndrome, d_bits_out, d_iters_out, d_synd_ok_out, d_posterior_out,
+                   (hipStream_t)stream);
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+int qldpc_decode_batch(qldpc_graph *g, const qldpc_params *p, int32_t batch, const double *llr,
+                       const uint8_t *syndrome, uint8_t *bits_out, uint32_t *iters_out, uint8_t *synd_ok_out,
+                       double *posterior_out) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch == 0) return QLDPC_OK;
+    if (!llr || !syndrome || !bits_out || !iters_out || !synd_ok_out) return fail(QLDPC_EINVAL, "NULL host buffer");
+    const int G = (int)g->devs.size();
+    const int per = (batch + G - 1) / G;
+    std::vector<int> rcs(G, QLDPC_OK);
+    std::vector<std::string> errs(G);
+    auto work = [&](int gi) {
+        DeviceGraph *dg = g->devs[gi].get();
+        const int f0 = gi * per, f1 = std::min(batch, f0 + per), nb = f1 - f0;
+        if (nb <= 0) return;
+        const size_t n = (size_t)g->n, m = (size_t)g->m;
+        auto body = [&]() -> int {
+            HIP_TRY(hipSetDevice(dg->device));
+            std::lock_guard<std::mutex> lk(dg->mu);  // the device's staging buffers
+            HostIO &io = dg->io;
+            if (!io.stream) HIP_TRY(hipStreamCreateWithFlags(&io.stream, hipStreamNonBlocking));
+            if ((size_t)nb > io.cap_frames) {
+                int r;
+                if ((r = grow(&io.llr, nb * n)) || (r = grow(&io.post, nb * n)) || (r = grow(&io.synd, nb * m)) ||
+                    (r = grow(&io.bits, nb * n)) || (r = grow(&io.ok, (size_t)nb)) || (r = grow(&io.iters, (size_t)nb)))
+                    return r;
+                io.cap_frames = (size_t)nb;
+            }
+            HIP_TRY(hipMemcpyAsync(io.llr, llr + f0 * n, nb * n * sizeof(double), hipMemcpyHostToDevice, io.stream));
+            HIP_TRY(hipMemcpyAsync(io.synd, syndrome + f0 * m, nb * m, hipMemcpyHostToDevice, io.stream));
+            return QLDPC_OK;
+        };
+        int r = body();
+        if (!r) {
+            HostIO &io = dg->io;
+            r = decode_on(g, dg, p, nb, io.llr, io.synd, io.bits, io.iters, io.ok, posterior_out ? io.post : nullptr,
+                          io.stream);
+            if (!r) {
+                auto fin = [&]() -> int {
+                    HIP_TRY(hipMemcpyAsync(bits_out + f0 * n, io.bits, nb * n, hipMemcpyDeviceToHost, io.stream));
+                    HIP_TRY(hipMemcpyAsync(iters_out + f0, io.iters, nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                           io.stream));
+                    HIP_TRY(hipMemcpyAsync(synd_ok_out + f0, io.ok, nb, hipMemcpyDeviceToHost, io.stream));
+                    if (posterior_out)
+                        HIP_TRY(hipMemcpyAsync(posterior_out + f0 * n, io.post, nb * n * sizeof(double),
+                                               hipMemcpyDeviceToHost, io.stream));
+                    HIP_TRY(hipStreamSynchronize(io.stream));
+                    return QLDPC_OK;
+                };
+                r = fin();
+            }
+        }
+        rcs[gi] = r;
+        if (r) errs[gi] = g_last_error;
+    };
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    if (G == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int gi = 0; gi < G; ++gi) th.emplace_back(work, gi);
+        for (auto &t : th) t.join();
+    }
+    (void)hipSetDevice(prev);
+    for (int gi = 0; gi < G; ++gi)
+        if (rcs[gi]) return fail(rcs[gi], errs[gi]);
+    return QLDPC_OK;
+}
+
+int qldpc_build_frames_device(qldpc_graph *g, int32_t device, int32_t batch, const uint8_t *d_alice,
+                              const uint8_t *d_bob, const double *d_log_p, double *d_llr, uint8_t *d_syndrome,
+                              void *stream) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch > 0 && (!d_alice || !d_bob || !d_log_p || !d_llr || !d_syndrome))
+        return fail(QLDPC_EINVAL, "NULL device buffer");
+    DeviceGraph *dg = find_dev(g, device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    hipError_t e = launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob,
+                                       d_log_p, d_llr, d_syndrome, (hipStream_t)stream);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return hip_fail(e, "build_frames");
+    return QLDPC_OK;
+}
+
+int qldpc_keys_match_device(int32_t batch, int32_t n, const uint8_t *d_alice, const uint8_t *d_bits,
+                            uint8_t *d_keys_match, void *stream) {
+    if (batch < 0 || n <= 0) return fail(QLDPC_EINVAL, "bad batch / n");
+    if (batch > 0 && (!d_alice || !d_bits || !d_keys_match)) return fail(QLDPC_EINVAL, "NULL device buffer");
+    hipError_t e = launch_keys_match(batch, n, d_alice, d_bits, d_keys_match, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "keys_match");
+    return QLDPC_OK;
+}
+
+int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream) {
+    if (fn < 0 || fn > 5 || count < 0) return fail(QLDPC_EINVAL, "fn must be 0..5, count >= 0");
+    if (count > 0 && (!d_in || !d_out)) return fail(QLDPC_EINVAL, "NULL device buffer");
+    hipError_t e = launch_math_selftest(fn, count, d_in, d_out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "math_selftest");
+    return QLDPC_OK;
+}
+
+int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_params *p, int32_t batch,
+                                const uint8_t *d_alice, const uint8_t *d_bob, const double *d_log_p,
+                                double *d_llr_ws, uint8_t *d_synd_ws, uint8_t *d_bits_out, uint32_t *d_iters_out,
+                                uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out, void *stream) {
+    int rc = qldpc_build_frames_device(g, device, batch, d_alice, d_bob, d_log_p, d_llr_ws, d_synd_ws, stream);
+    if (rc) return rc;
+    rc = qldpc_decode_batch_device(g, device, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out,
+                                   nullptr, stream);
+    if (rc) return rc;
+    if (!d_keys_match_out) return QLDPC_OK;
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    rc = qldpc_keys_match_device(batch, g->n, d_alice, d_bits_out, d_keys_match_out, stream);
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,541 @@
+// decoder.hip — gfx950 flooding belief-propagation decoder for QKD-LDPC.
+//
+// Hot path of ColdCloudd/QKD_LDPC_V: the six decoders of
+// src/qkd_ldpc_algorithm.cpp:3-1029 (SPA :3-144, SPA-linear :174-315,
+// NMSA :317-482, OMSA :484-650, ANMSA :652-839, AOMSA :841-1029), batched over
+// independent frames.  Results are bit-identical to the reference: same IEEE
+// operation sequence per message (no FMA contraction: built with
+// -ffp-contract=off), glibc-exact tanh/atanh (exact_math.h), the reference's
+// row-order products and std::accumulate-order sums.
+//
+// Mapping to the machine:
+//   * one workgroup decodes one frame at a time; workgroups are persistent and
+//     pull frame ids from a device counter, so an early-exiting frame frees its
+//     CU at once (frames converge after 3..50 iterations);
+//   * the frame's E edges are dealt to the T lanes in CSR (row-major) order,
+//     EPL consecutive edges per lane; the lane keeps those edges' messages in
+//     VGPRs across iterations (variant REG_LDS) or in a coalesced slot-major
+//     per-workgroup scratch (GLB_*);
+//   * posterior totals live in LDS (REG_LDS, GLB_LDS): every gather of a bit's
+//     total is an LDS read, never a scattered HBM read;
+//   * a row may straddle two lanes: its sequential product (SPA) or min1/min2
+//     aggregate (min-sum) is carried across the boundary through LDS;
+//   * variable-node sums are accumulated in the reference's order
+//     ((llr + c0) + c1) + ... by dv_max phases: phase k adds the message of every
+//     edge that is the k-th edge of its bit.
+#include <float.h>
+
+#include "decoder.hpp"
+#include "exact_math.h"
+
+namespace qldpc {
+
+namespace {
+
+// threshold_matrix (src/array_and_matrix_operations.cpp:953-972): NaN passes.
+__device__ __forceinline__ double clip_msg(double v, double thr) {
+    if (v > thr) return thr;
+    if (v < -thr) return -thr;
+    return v;
+}
+
+// tanh_lin_approx / atanh_lin_approx (src/qkd_ldpc_algorithm.cpp:146-172).
+__device__ __forceinline__ double tanh_lin(double x) {
+    const double a = fabs(x);
+    double r;
+    if (a < 0.5) r = 0.9242 * a;
+    else if (a < 0.9) r = 0.6355 * a + 0.1444;
+    else if (a < 1.2) r = 0.3912 * a + 0.3642;
+    else if (a < 1.75) r = 0.1958 * a + 0.5986;
+    else if (a < 2.5) r = 0.0603 * a + 0.8358;
+    else if (a < 3.5) r = 0.0115 * a + 0.9577;
+    else if (a < 8) r = 0.0004 * a + 0.9967;
+    else r = 1;
+    return (x < 0.) ? -r : r;
+}
+__device__ __forceinline__ double atanh_lin(double x) {
+    const double a = fabs(x);
+    double r;
+    if (a < 0.7) r = 1.196 * a - 0.0323;
+    else if (a < 0.9) r = 2.9187 * a - 1.214;
+    else if (a < 0.999) r = 10.8717 * a - 8.3717;
+    else r = 2510.9 * a - 2505.9;
+    return (x < 0.) ? -r : r;
+}
+
+// Min-sum row aggregate: parity of x<0, and the two smallest |x| with the
+// reference's strict-< scan (src/qkd_ldpc_algorithm.cpp:381-397).  The scan's
+// result is the two smallest of {|x| : |x| < DBL_MAX} padded with DBL_MAX, so
+// partial aggregates merge order-free (exact).
+struct MinAgg {
+    double m1, m2;
+    int neg;
+};
+__device__ __forceinline__ void agg_init(MinAgg &a) {
+    a.m1 = DBL_MAX;
+    a.m2 = DBL_MAX;
+    a.neg = 0;
+}
+__device__ __forceinline__ void agg_push(MinAgg &a, double x) {
+    if (x < 0) a.neg ^= 1;
+    const double ax = fabs(x);
+    if (ax < a.m1) {
+        a.m2 = a.m1;
+        a.m1 = ax;
+    } else if (ax < a.m2) {
+        a.m2 = ax;
+    }
+}
+__device__ __forceinline__ void agg_merge(MinAgg &a, const MinAgg &b) {
+    a.neg ^= b.neg;
+    const bool bl = b.m1 < a.m1;
+    const double lo = bl ? b.m1 : a.m1;
+    const double hi = bl ? a.m1 : b.m1;
+    const double m2 = (a.m2 < b.m2) ? a.m2 : b.m2;
+    a.m1 = lo;
+    a.m2 = (hi < m2) ? hi : m2;
+}
+
+// Per-edge message storage of one lane.
+template <int R>
+struct EdgeMsgs {  // VGPR-resident: R slots, indexed only by unrolled constants
+    double v[R];
+    __device__ __forceinline__ void bind(double *, int, int) {}
+    __device__ __forceinline__ double get(int k) const { return v[k]; }
+    __device__ __forceinline__ void set(int k, double x) { v[k] = x; }
+};
+template <>
+struct EdgeMsgs<0> {  // per-workgroup global scratch, slot-major [k][lane]: coalesced
+    double *p;
+    int T;
+    __device__ __forceinline__ void bind(double *base, int tid, int TT) {
+        p = base + tid;
+        T = TT;
+    }
+    __device__ __forceinline__ double get(int k) const { return p[(size_t)k * T]; }
+    __device__ __forceinline__ void set(int k, double x) { p[(size_t)k * T] = x; }
+};
+
+// Visit this lane's slots in order, handing each slot's metadata word to f.
+// Metadata is one uint4 per four consecutive slots, group-major [g][lane], so a
+// wave reads 1 KiB contiguous per group.  The register variant uses a fixed
+// group stride of REG_TSTRIDE lanes and buffer loads whose group offset is a
+// compile-time constant: no per-group address stays live across the kernel.
+#ifdef QL_SLOT_FENCE
+#define QL_SLOT_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define QL_SLOT_BARRIER() ((void)0)
+#endif
+
+template <int R>
+struct MetaSrc {
+    __amdgpu_buffer_rsrc_t rs;
+    int voff;
+    __device__ __forceinline__ void init(const uint32_t *base, int tid, int) {
+        rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (R / 4) * REG_TSTRIDE * 16, 0x00020000);
+        voff = tid * 16;
+    }
+    template <typename F>
+    __device__ __forceinline__ void each(int, F &&f) const {
+        static_assert(R % 4 == 0, "register slots come in groups of four");
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, g * REG_TSTRIDE * 16, 0);
+            f(4 * g + 0, (uint32_t)q[0]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 1, (uint32_t)q[1]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 2, (uint32_t)q[2]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 3, (uint32_t)q[3]);
+            QL_SLOT_BARRIER();
+        }
+    }
+};
+template <>
+struct MetaSrc<0> {
+    const uint4 *mp;
+    int T;
+    __device__ __forceinline__ void init(const uint32_t *base, int tid, int TT) {
+        mp = reinterpret_cast<const uint4 *>(base) + tid;
+        T = TT;
+    }
+    template <typename F>
+    __device__ __forceinline__ void each(int EPL, F &&f) const {
+        const int G = (EPL + 3) >> 2;
+        for (int g = 0; g < G; ++g) {
+            const uint4 q = mp[(size_t)g * T];
+            f(4 * g + 0, q.x);
+            f(4 * g + 1, q.y);
+            f(4 * g + 2, q.z);
+            f(4 * g + 3, q.w);
+        }
+    }
+};
+
+constexpr int CTRL_BYTES = 16;
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// Byte layout of the per-frame state block (LDS or global scratch).
+struct FrameLayout {
+    size_t total, rowA, rowB, carryA, carryB, carryI, rowflag, bytes;
+    __host__ __device__ FrameLayout(int n, int m, int T) {
+        size_t o = 0;
+        total = o; o = align16(o + (size_t)n * 8);
+        rowA = o; o = align16(o + (size_t)m * 8);
+        rowB = o; o = align16(o + (size_t)m * 8);
+        carryA = o; o = align16(o + (size_t)T * 8);
+        carryB = o; o = align16(o + (size_t)T * 8);
+        carryI = o; o = align16(o + (size_t)T * 4);
+        rowflag = o; o = align16(o + (size_t)m);
+        bytes = o;
+    }
+};
+
+template <int ALG, int R, bool TOT_LDS>
+__global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
+    constexpr bool ADAPT = (ALG == 4 || ALG == 5);
+    constexpr bool NORM = (ALG == 2 || ALG == 4);
+
+    const int tid = threadIdx.x;
+    const int T = a.T, n = a.n, m = a.m, EPL = a.EPL;
+    const double thr = a.thr;
+    const bool thr_on = a.thr_on != 0;
+
+    double *wg = a.scratch ? a.scratch + (size_t)blockIdx.x * (size_t)a.scratch_wg_doubles : nullptr;
+    const FrameLayout L(n, m, T);
+    unsigned char *fb;
+    if constexpr (TOT_LDS) fb = smem + CTRL_BYTES;
+    else fb = reinterpret_cast<unsigned char *>(wg + (R == 0 ? (size_t)EPL * T : 0));
+    double *total = reinterpret_cast<double *>(fb + L.total);
+    double *rowA = reinterpret_cast<double *>(fb + L.rowA);
+    double *rowB = reinterpret_cast<double *>(fb + L.rowB);
+    double *carryA = reinterpret_cast<double *>(fb + L.carryA);
+    double *carryB = reinterpret_cast<double *>(fb + L.carryB);
+    int *carryI = reinterpret_cast<int *>(fb + L.carryI);
+    uint8_t *rowflag = fb + L.rowflag;  // bit0 target syndrome, bit1 row mismatch, bit2 neg parity
+    int *s_frame = reinterpret_cast<int *>(smem);
+
+    EdgeMsgs<R> c2b;
+    if constexpr (R == 0) c2b.bind(wg, tid, T);
+
+    MetaSrc<R> meta;
+    meta.init(a.slot_meta, tid, T);
+    const int head_in = a.lane_head[tid];
+    const int row0_in = a.lane_row0[tid];
+
+    for (;;) {
+        if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        __syncthreads();
+        const int f = *s_frame;
+        if (f >= a.batch) break;
+        const double *llr = a.llr + (size_t)f * n;
+        const uint8_t *sy = a.synd + (size_t)f * m;
+        for (int j = tid; j < m; j += T) rowflag[j] = sy[j] & 1;
+        if constexpr (ADAPT)
+            for (int i = tid; i < n; i += T) total[i] = 0.0;  // total_bit_llr starts zeroed
+        __syncthreads();
+
+        int iters = a.max_it, okv = 0;
+        bool had_vn = false;
+        for (int it = 0;; ++it) {
+            // ---- syndrome check of the current decision --------------------------
+            // SPA/SPA-lin/NMSA/OMSA: after each VN (:86,101-107), so at the top of
+            // it >= 1 and once more after the last iteration.  ANMSA/AOMSA: inside
+            // the CN pass of every iteration, on the previous decisions (:745-776).
+            const bool needS = ADAPT ? (it < a.max_it) : (it > 0);
+            if (needS) {
+                int mis = 0;
+                for (int j = tid; j < m; j += T) {
+                    const int deg = a.row_deg[j];
+                    int par = 0;
+                    for (int k = 0; k < deg; ++k) {
+                        const int c = a.ell_col[(size_t)k * m + j];
+                        const double z = had_vn ? total[c] : llr[c];
+                        par ^= (z <= 0.0) ? 1 : 0;
+                    }
+                    const uint8_t fl = rowflag[j];
+                    const int rm = (par ^ fl) & 1;
+                    rowflag[j] = (uint8_t)((fl & 5) | (rm << 1));
+                    mis |= rm;
+                }
+                if (!__syncthreads_or(mis)) {
+                    iters = ADAPT ? it + 1 : it;
+                    okv = 1;
+                    break;
+                }
+            }
+            if (it == a.max_it) break;
+
+            // Re-opaque the lane constants each iteration: per-slot masks derived
+            // from them (k < head, ...) are then computed at their use instead
+            // of being hoisted out of the frame loop into ~80 SGPRs.
+            int head = head_in, row0 = row0_in;
+            asm volatile("" : "+v"(head), "+v"(row0));
+
+            // ---- CN phase 1: b2c, tanh / row aggregates over this lane's edges ----
+            int r = row0;
+            double acc = 0.0;
+            MinAgg ag, hag;
+            agg_init(ag);
+            agg_init(hag);
+            bool tail_open = false;
+            meta.each(EPL, [&](int k, uint32_t mt) {
+                if (!(mt & META_VALID)) return;
+                if (k > 0 && (mt & META_START)) ++r;
+                const int col = (int)(mt & META_COL_MASK);
+                double x;
+                if (it == 0) {
+                    x = llr[col];  // initial b2c = channel LLR, unclipped (:21-29)
+                } else {
+                    x = total[col] - c2b.get(k);  // VN extrinsic (:115)
+                    if (thr_on) x = clip_msg(x, thr);
+                }
+                if constexpr (SPA_FAM) {
+                    const double t = (ALG == 0) ? ql_exact::tanh_exact(x / 2.) : tanh_lin(x / 2.);
+                    c2b.set(k, t);
+                    if (k < head) return;
+                    if (mt & META_START) acc = ((rowflag[r] & 1) ? -1. : 1.) * t;  // :57-62
+                    else acc = acc * t;
+                    if (mt & META_END) rowA[r] = acc;
+                    tail_open = !(mt & META_END);
+                } else {
+                    c2b.set(k, x);
+                    if (k < head) {
+                        agg_push(hag, x);
+                        return;
+                    }
+                    if (mt & META_START) agg_init(ag);
+                    agg_push(ag, x);
+                    if (mt & META_END) {
+                        rowA[r] = ag.m1;
+                        rowB[r] = ag.m2;
+                        rowflag[r] = (uint8_t)((rowflag[r] & 3) | (ag.neg << 2));
+                    }
+                    tail_open = !(mt & META_END);
+                }
+            });
+            if (tail_open) {
+                if constexpr (SPA_FAM) {
+                    carryA[tid] = acc;
+                } else {
+                    carryA[tid] = ag.m1;
+                    carryB[tid] = ag.m2;
+                    carryI[tid] = ag.neg;
+                }
+            }
+            __syncthreads();
+
+            // ---- CN phase 2: finish rows begun in the previous lane ----------------
+            if (head > 0) {
+                if constexpr (SPA_FAM) {
+                    double p = carryA[tid - 1];
+                    if constexpr (R > 0) {
+#pragma unroll
+                        for (int k = 0; k < R; ++k)
+                            if (k < head) p = p * c2b.get(k);
+                    } else {
+                        for (int k = 0; k < head; ++k) p = p * c2b.get(k);
+                    }
+                    rowA[row0] = p;
+                } else {
+                    MinAgg t;
+                    t.m1 = carryA[tid - 1];
+                    t.m2 = carryB[tid - 1];
+                    t.neg = carryI[tid - 1];
+                    agg_merge(t, hag);
+                    rowA[row0] = t.m1;
+                    rowB[row0] = t.m2;
+                    rowflag[row0] = (uint8_t)((rowflag[row0] & 3) | (t.neg << 2));
+                }
+            }
+            __syncthreads();
+
+            // ---- CN phase 3: check-to-bit messages, clipped (:64-74 etc.) ---------
+            r = row0;
+            meta.each(EPL, [&](int k, uint32_t mt) {
+                if (!(mt & META_VALID)) return;
+                if (k > 0 && (mt & META_START)) ++r;
+                double c;
+                if constexpr (SPA_FAM) {
+                    const double prod = rowA[r] / c2b.get(k);  // :66
+                    c = 2. * ((ALG == 0) ? ql_exact::atanh_exact(prod) : atanh_lin(prod));
+                } else {
+                    const double x = c2b.get(k);
+                    const uint8_t fl = rowflag[r];
+                    double sp = (fl & 1) ? -1. : 1.;  // :376
+                    sp *= ((fl >> 2) & 1) ? -1. : 1.;  // :398
+                    const double prod = sp * ((x > 0) ? 1. : -1.);  // :402
+                    const double m1 = rowA[r];
+                    const double sel = (fabs(x) == m1) ? rowB[r] : m1;  // :406
+                    double fac = a.primary;
+                    if (ADAPT && (fl & 2)) fac = a.secondary;  // :749-757
+                    if constexpr (NORM) {
+                        c = fac * prod * sel;  // :405-406
+                    } else {
+                        const double d = sel - fac;  // :573-574
+                        c = prod * ((d < 0.) ? 0. : d);
+                    }
+                }
+                if (thr_on) c = clip_msg(c, thr);
+                c2b.set(k, c);
+            });
+
+            // ---- VN: totals in std::accumulate order (:76-84) -----------------------
+            for (int i = tid; i < n; i += T) total[i] = llr[i];
+            __syncthreads();
+            for (int kk = 0; kk < a.dv_max; ++kk) {
+                meta.each(EPL, [&](int k, uint32_t mt) {
+                    if ((mt & META_VALID) && ((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
+                        const int col = (int)(mt & META_COL_MASK);
+                        total[col] = total[col] + c2b.get(k);
+                    }
+                });
+                __syncthreads();
+            }
+            had_vn = true;
+        }
+
+        // ---- outputs: bit_array_out, decoding_result, total_bit_llr ----------------
+        uint8_t *bits = a.bits + (size_t)f * n;
+        double *post = a.post ? a.post + (size_t)f * n : nullptr;
+        for (int i = tid; i < n; i += T) {
+            const double z = had_vn ? total[i] : llr[i];
+            bits[i] = (z <= 0.0) ? 1 : 0;
+            if (post) post[i] = total[i];
+        }
+        if (tid == 0) {
+            a.iters[f] = (uint32_t)iters;
+            a.ok[f] = (uint8_t)okv;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- QKD_LDPC frame construction (src/qkd_ldpc_algorithm.cpp:1043-1052) --------
+__global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const int32_t *ell_col,
+                                                           const int32_t *row_deg, const uint8_t *alice,
+                                                           const uint8_t *bob, const double *log_p,
+                                                           double *llr, uint8_t *synd) {
+    const size_t f = blockIdx.x;
+    const double lp = log_p[f];
+    const uint8_t *al = alice + f * (size_t)n;
+    const uint8_t *bo = bob + f * (size_t)n;
+    double *l = llr + f * (size_t)n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) l[i] = bo[i] ? -lp : lp;
+    uint8_t *s = synd + f * (size_t)m;
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        int p = 0;
+        const int deg = row_deg[j];
+        for (int k = 0; k < deg; ++k) p ^= al[ell_col[(size_t)k * m + j]];
+        s[j] = (uint8_t)(p & 1);
+    }
+}
+
+// keys_match = arrays_equal(alice, bob_solution) (src/qkd_ldpc_algorithm.cpp:1087).
+__global__ void __launch_bounds__(256) keys_match_kernel(int n, const uint8_t *alice, const uint8_t *bits,
+                                                         uint8_t *match) {
+    const size_t f = blockIdx.x;
+    int diff = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) diff |= (alice[f * n + i] != bits[f * n + i]);
+    diff = __syncthreads_or(diff);
+    if (threadIdx.x == 0) match[f] = diff ? 0 : 1;
+}
+
+__global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, const double *in, double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const double x = in[i];
+    double y;
+    switch (fn) {
+    case 0: y = ql_exact::tanh_exact(x); break;
+    case 1: y = ql_exact::atanh_exact(x); break;
+    case 2: y = ql_exact::expm1_exact(x); break;
+    case 3: y = ql_exact::log1p_exact(x); break;
+    case 4: y = tanh_lin(x); break;
+    default: y = atanh_lin(x); break;
+    }
+    out[i] = y;
+}
+
+using KernelFn = void (*)(DecodeArgs);
+
+template <int ALG>
+KernelFn pick(int variant) {
+    switch (variant) {
+    case VAR_REG_LDS: return decode_kernel<ALG, EPL_REG, true>;
+    case VAR_GLB_LDS: return decode_kernel<ALG, 0, true>;
+    default: return decode_kernel<ALG, 0, false>;
+    }
+}
+
+KernelFn kernel_for(int variant, int alg) {
+    switch (alg) {
+    case 0: return pick<0>(variant);
+    case 1: return pick<1>(variant);
+    case 2: return pick<2>(variant);
+    case 3: return pick<3>(variant);
+    case 4: return pick<4>(variant);
+    default: return pick<5>(variant);
+    }
+}
+
+}  // namespace
+
+size_t lds_bytes_for(int variant, int n, int m, int T) {
+    if (variant == VAR_GLB_GLB) return CTRL_BYTES;
+    return CTRL_BYTES + FrameLayout(n, m, T).bytes;
+}
+
+long long scratch_doubles_for(int variant, int n, int m, int T, int EPL) {
+    long long d = 0;
+    if (variant != VAR_REG_LDS) d += (long long)EPL * T;
+    if (variant == VAR_GLB_GLB) d += (long long)((FrameLayout(n, m, T).bytes + 7) / 8);
+    return d;
+}
+
+hipError_t launch_decode(int variant, const DecodeArgs &a, int workgroups, size_t lds_bytes,
+                         hipStream_t stream) {
+    KernelFn k = kernel_for(variant, a.alg);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(workgroups), dim3(a.T), lds_bytes, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
+    KernelFn k = kernel_for(variant, alg);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, T, lds_bytes);
+}
+
+hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
+                               int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
+                               double *llr, uint8_t *synd, hipStream_t stream) {
+    (void)max_dc;
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, alice,
+                       bob, log_p, llr, synd);
+    return hipGetLastError();
+}
+
+hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(math_selftest_kernel, dim3((count + 255) / 256), dim3(256), 0, stream, fn, count, in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits, uint8_t *match,
+                             hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(keys_match_kernel, dim3(batch), dim3(256), 0, stream, n, alice, bits, match);
+    return hipGetLastError();
+}
+
+}  // namespace qldpc

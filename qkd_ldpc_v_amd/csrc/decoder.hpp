@@ -1,0 +1,71 @@
+// decoder.hpp — host/device shared definitions of the gfx950 LDPC decoder.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qldpc {
+
+// Per-slot metadata word (slot-major [slot][lane], one uint32 per CSR edge).
+constexpr uint32_t META_COL_MASK = 0xFFFFFu;   // bit id (n <= 2^20)
+constexpr int META_KPOS_SHIFT = 20;            // position of the edge in its bit's check list
+constexpr uint32_t META_KPOS_MASK = 0x3Fu;     // dv <= 64
+constexpr uint32_t META_START = 1u << 26;      // first edge of its row
+constexpr uint32_t META_END = 1u << 27;        // last edge of its row
+constexpr uint32_t META_VALID = 1u << 28;      // slot holds an edge (tail padding otherwise)
+constexpr int MAX_DV = 64;
+constexpr int MAX_N = 1 << 20;
+
+// Registers available for per-edge messages in the register-resident variant.
+constexpr int EPL_REG = 40;
+// Lane stride of the register variant's metadata groups (== max lanes).
+constexpr int REG_TSTRIDE = 1024;
+
+enum Variant : int {
+    VAR_REG_LDS = 0,  // messages in VGPRs, totals/rows in LDS       (n <~ 14k)
+    VAR_GLB_LDS = 1,  // messages in per-workgroup global scratch, totals/rows in LDS
+    VAR_GLB_GLB = 2,  // everything per-frame in global scratch     (n = 100k)
+};
+
+struct DecodeArgs {
+    // graph (device pointers; shared by every frame)
+    int n, m, E, T, EPL, dv_max, max_dc;
+    const uint32_t *slot_meta;  // [ceil(EPL/4)][T][4]: uint4 per 4 slots
+    const int32_t *lane_row0;   // [T] row of slot 0 (or -1)
+    const int32_t *lane_head;   // [T] leading slots that finish a row begun in lane-1
+    const int32_t *ell_col;     // [max_dc][m] bit ids of each row, row-ELL, slot-major
+    const int32_t *row_deg;     // [m]
+    // decoder parameters
+    int alg, max_it, thr_on;
+    double thr, primary, secondary;
+    // frames
+    int batch;
+    const double *llr;      // [batch][n]
+    const uint8_t *synd;    // [batch][m]
+    uint8_t *bits;          // [batch][n]
+    uint32_t *iters;        // [batch]
+    uint8_t *ok;            // [batch]
+    double *post;           // [batch][n] or nullptr
+    // scheduling / scratch
+    int *frame_counter;
+    double *scratch;              // per-workgroup scratch (variants 1, 2)
+    long long scratch_wg_doubles; // doubles per workgroup
+};
+
+// Dynamic LDS bytes / scratch doubles a variant needs for this shape.
+size_t lds_bytes_for(int variant, int n, int m, int T);
+long long scratch_doubles_for(int variant, int n, int m, int T, int EPL);
+
+// Launch the persistent decoder: grid = `workgroups`, block = args.T.
+hipError_t launch_decode(int variant, const DecodeArgs &a, int workgroups, size_t lds_bytes,
+                         hipStream_t stream);
+// Max resident workgroups per CU for (variant, alg, T, lds).
+hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
+
+hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
+                               int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
+                               double *llr, uint8_t *synd, hipStream_t stream);
+hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
+hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
+                             uint8_t *match, hipStream_t stream);
+
+}  // namespace qldpc

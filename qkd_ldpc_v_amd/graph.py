@@ -1,0 +1,192 @@
+"""Parity-check matrices and device graphs.
+
+HMatrix mirrors the reference's H_matrix (src/array_and_matrix_operations.hpp:
+60-77) as flat CSR (check_nodes) + CSC (bit_nodes) arrays; load_matrix() calls
+the C ABI's reader, which restates the reference's four file formats.
+Graph owns a qldpc_graph: the decoder's lane partition, replicated on devices.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import Params, check, lib, ptr
+
+
+@dataclass
+class HMatrix:
+    n: int
+    m: int
+    row_ptr: np.ndarray  # int32[m+1] check_nodes
+    col_idx: np.ndarray  # int32[nnz]
+    col_ptr: np.ndarray  # int32[n+1] bit_nodes
+    row_idx: np.ndarray  # int32[nnz]
+    is_regular: bool = False
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row_ptr[-1])
+
+    @property
+    def check_nodes(self) -> list[list[int]]:
+        rp, ci = self.row_ptr, self.col_idx
+        return [ci[rp[j]:rp[j + 1]].tolist() for j in range(self.m)]
+
+    @property
+    def bit_nodes(self) -> list[list[int]]:
+        cp, ri = self.col_ptr, self.row_idx
+        return [ri[cp[i]:cp[i + 1]].tolist() for i in range(self.n)]
+
+    @property
+    def code_rate(self) -> float:
+        """1 - M/N (reference src/simulation.cpp:389)."""
+        return 1.0 - self.m / self.n
+
+    @classmethod
+    def from_check_nodes(cls, n: int, check_nodes: list[list[int]]) -> "HMatrix":
+        """H from per-check bit lists; bit_nodes is the ascending transpose."""
+        m = len(check_nodes)
+        row_ptr = np.zeros(m + 1, np.int32)
+        row_ptr[1:] = np.cumsum([len(r) for r in check_nodes])
+        col_idx = np.array([c for r in check_nodes for c in r], np.int32)
+        order = np.lexsort((np.repeat(np.arange(m), np.diff(row_ptr)), col_idx))
+        row_idx = np.repeat(np.arange(m, dtype=np.int32), np.diff(row_ptr))[order]
+        col_ptr = np.zeros(n + 1, np.int32)
+        col_ptr[1:] = np.cumsum(np.bincount(col_idx, minlength=n))
+        return cls(n, m, row_ptr, col_idx, col_ptr, row_idx.astype(np.int32), False)
+
+    def syndrome(self, bits: np.ndarray) -> np.ndarray:
+        """calculate_syndrome over the last axis (src/array_and_matrix_operations.cpp:936-950)."""
+        b = np.asarray(bits, np.uint8)
+        vals = b[..., self.col_idx].astype(np.int64)
+        cs = np.concatenate([np.zeros(b.shape[:-1] + (1,), np.int64), np.cumsum(vals, axis=-1)], axis=-1)
+        return ((cs[..., self.row_ptr[1:]] - cs[..., self.row_ptr[:-1]]) & 1).astype(np.uint8)
+
+
+def load_matrix(path: str, fmt: int) -> HMatrix:
+    """Read a matrix file in reference format `fmt` (0 uncompressed, 1 alist, 2 sparse_1, 3 sparse_2)."""
+    L = lib()
+    n, m, nnz, reg = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    p = str(path).encode()
+    check(L.qldpc_load_matrix(p, fmt, ctypes.byref(n), ctypes.byref(m), ctypes.byref(nnz), None, None, None, None,
+                              ctypes.byref(reg)), f"qldpc_load_matrix({path})")
+    rp = np.empty(m.value + 1, np.int32)
+    ci = np.empty(nnz.value, np.int32)
+    cp = np.empty(n.value + 1, np.int32)
+    ri = np.empty(nnz.value, np.int32)
+    check(L.qldpc_load_matrix(p, fmt, ctypes.byref(n), ctypes.byref(m), ctypes.byref(nnz), ptr(rp), ptr(ci), ptr(cp),
+                              ptr(ri), ctypes.byref(reg)), f"qldpc_load_matrix({path})")
+    return HMatrix(n.value, m.value, rp, ci, cp, ri, bool(reg.value))
+
+
+@dataclass
+class DecodeOutput:
+    bits: np.ndarray        # uint8[batch, n]  bit_array_out
+    iterations: np.ndarray  # uint32[batch]    decoding_result.iterations_num
+    synd_ok: np.ndarray     # uint8[batch]     decoding_result.syndromes_match
+    posterior: np.ndarray | None  # float64[batch, n] total_bit_llr
+
+
+class Graph:
+    """A device-resident Tanner graph (qldpc_graph)."""
+
+    def __init__(self, H: HMatrix, device_mask: int = 0):
+        self.H = H
+        self.n, self.m = H.n, H.m
+        g = ctypes.c_void_p()
+        check(lib().qldpc_graph_create_checked(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(H.col_ptr),
+                                               ptr(H.row_idx), int(device_mask), ctypes.byref(g)),
+              "qldpc_graph_create_checked")
+        self._g = g
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._g
+
+    def close(self) -> None:
+        if getattr(self, "_g", None) is not None and self._g.value:
+            lib().qldpc_graph_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> dict:
+        n, m, nnz, nd = (ctypes.c_int32() for _ in range(4))
+        check(lib().qldpc_graph_info(self._g, ctypes.byref(n), ctypes.byref(m), ctypes.byref(nnz), ctypes.byref(nd)),
+              "qldpc_graph_info")
+        return {"n": n.value, "m": m.value, "nnz": nnz.value, "devices": nd.value}
+
+    def plan(self, device: int = 0, algorithm: int = 0) -> dict:
+        lanes, epl, wgs, lds = (ctypes.c_int32() for _ in range(4))
+        var = ctypes.c_char_p()
+        check(lib().qldpc_graph_plan(self._g, device, algorithm, ctypes.byref(lanes), ctypes.byref(epl),
+                                     ctypes.byref(wgs), ctypes.byref(lds), ctypes.byref(var)), "qldpc_graph_plan")
+        return {"lanes": lanes.value, "edges_per_lane": epl.value, "workgroups": wgs.value,
+                "lds_bytes": lds.value, "variant": var.value.decode()}
+
+    # ---- host-buffer decode (synchronous, shards over the graph's devices) ----
+    def decode(self, params: Params, llr: np.ndarray, syndrome: np.ndarray, posterior: bool = False) -> DecodeOutput:
+        llr = np.ascontiguousarray(llr, np.float64)
+        syn = np.ascontiguousarray(syndrome, np.uint8)
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        if syn.ndim == 1:
+            syn = syn[None, :]
+        batch = llr.shape[0]
+        if llr.shape != (batch, self.n) or syn.shape != (batch, self.m):
+            raise ValueError(f"expected llr ({batch},{self.n}) and syndrome ({batch},{self.m})")
+        bits = np.empty((batch, self.n), np.uint8)
+        iters = np.empty(batch, np.uint32)
+        ok = np.empty(batch, np.uint8)
+        post = np.empty((batch, self.n), np.float64) if posterior else None
+        p = params.c()
+        check(lib().qldpc_decode_batch(self._g, ctypes.byref(p), batch, ptr(llr), ptr(syn), ptr(bits), ptr(iters),
+                                       ptr(ok), ptr(post)), "qldpc_decode_batch")
+        return DecodeOutput(bits, iters, ok, post)
+
+    # ---- device-pointer entries (torch tensors as plumbing) ----
+    def decode_device(self, params: Params, llr, syndrome, bits, iters, ok, posterior=None, stream=None,
+                      device: int | None = None) -> None:
+        dev = llr.device.index if device is None else device
+        p = params.c()
+        check(lib().qldpc_decode_batch_device(
+            self._g, dev, ctypes.byref(p), int(llr.shape[0]), llr.data_ptr(), syndrome.data_ptr(), bits.data_ptr(),
+            iters.data_ptr(), ok.data_ptr(), None if posterior is None else posterior.data_ptr(),
+            _stream_ptr(stream, dev)), "qldpc_decode_batch_device")
+
+    def build_frames_device(self, alice, bob, log_p, llr, syndrome, stream=None, device: int | None = None) -> None:
+        dev = alice.device.index if device is None else device
+        check(lib().qldpc_build_frames_device(self._g, dev, int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(),
+                                              log_p.data_ptr(), llr.data_ptr(), syndrome.data_ptr(),
+                                              _stream_ptr(stream, dev)), "qldpc_build_frames_device")
+
+    def qkd_ldpc_device(self, params: Params, alice, bob, log_p, llr_ws, synd_ws, bits, iters, ok, keys_match,
+                        stream=None, device: int | None = None) -> None:
+        """QKD_LDPC's per-trial window for a batch, all on device."""
+        dev = alice.device.index if device is None else device
+        p = params.c()
+        check(lib().qldpc_qkd_ldpc_batch_device(
+            self._g, dev, ctypes.byref(p), int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(), log_p.data_ptr(),
+            llr_ws.data_ptr(), synd_ws.data_ptr(), bits.data_ptr(), iters.data_ptr(), ok.data_ptr(),
+            keys_match.data_ptr(), _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_batch_device")
+
+
+def keys_match_device(alice, bits, out, stream=None) -> None:
+    dev = alice.device.index
+    check(lib().qldpc_keys_match_device(int(alice.shape[0]), int(alice.shape[1]), alice.data_ptr(), bits.data_ptr(),
+                                        out.data_ptr(), _stream_ptr(stream, dev)), "qldpc_keys_match_device")
+
+
+def _stream_ptr(stream, device: int):
+    if stream is None:
+        import torch
+
+        return torch.cuda.current_stream(device).cuda_stream
+    return getattr(stream, "cuda_stream", stream)
