@@ -23,6 +23,17 @@ $(CSRC)/loaders.o: $(CSRC)/loaders.cpp $(CSRC)/loaders.hpp
 $(LIB): $(CSRC)/decoder.o $(CSRC)/capi.o $(CSRC)/loaders.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
+# Diagnostic build with per-phase s_memtime stamps (never the product).
+STAMPLIB := $(PKG)/diag/libqkdldpc_hip.so
+stamps: $(STAMPLIB)
+$(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
+$(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
+	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
+$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
+	mkdir -p $(PKG)/diag
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
+
 $(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h
 	$(MAKE) -C oracle
 
@@ -30,7 +41,7 @@ $(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp
 	g++ -O2 -std=c++17 -Wall -I include $< -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/..' -o $@
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK)
+	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK) $(STAMPLIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean
+.PHONY: all clean stamps

@@ -160,8 +160,9 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
 
 /* Diagnostic: evaluate the decoder's device math on `count` inputs on the
  * current device — fn 0 tanh, 1 atanh, 2 expm1, 3 log1p (exact_math.h, the
- * glibc-exact restatement used by the SPA kernel), 4 tanh_lin_approx,
- * 5 atanh_lin_approx (src/qkd_ldpc_algorithm.cpp:146-172). */
+ * glibc-exact restatement), 4 tanh_lin_approx, 5 atanh_lin_approx
+ * (src/qkd_ldpc_algorithm.cpp:146-172), 6 tanh and 7 atanh in the decoder
+ * forms the SPA kernel calls. */
 int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream);
 
 /* Thread-local description of the last failure on this thread. */

@@ -15,6 +15,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqkdldpc_hip.so")
+if os.environ.get("QLDPC_DIAG_STAMPS") == "1":  # diagnostic phase-stamp build (Makefile target `stamps`)
+    LIB_PATH = os.path.join(_HERE, "diag", "libqkdldpc_hip.so")
 
 QLDPC_OK = 0
 ERROR_NAMES = {-1: "EINVAL", -2: "EHIP", -3: "EIO", -4: "ENOMEM", -5: "EUNSUP"}

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -90,36 +91,26 @@ const char *variant_name(int v) {
 
 int round_up64(long long x) { return (int)(((x + 63) / 64) * 64); }
 
-// Choose (variant, T, EPL).  max_dc <= EPL keeps any row within two lanes.
+// Choose (variant, T, EPL).  EPL >= max_dc keeps any row within two lanes;
+// lanes past the last edge simply hold no slots.
 void plan(qldpc_graph &g) {
     const long long E = g.E;
-    // Register-resident messages: EPL_REG edges per lane at most.
-    {
-        int T = std::max(64, round_up64((E + EPL_REG - 1) / EPL_REG));
-        if (T <= 1024) {
-            int EPL = (int)((E + T - 1) / T);
-            if (EPL < 1) EPL = 1;
-            while (g.max_dc > EPL && T > 64) {
-                T -= 64;
-                EPL = (int)((E + T - 1) / T);
-            }
-            if (g.max_dc <= EPL && EPL <= EPL_REG && lds_bytes_for(VAR_REG_LDS, g.n, g.m, T) <= LDS_LIMIT) {
-                g.variant = VAR_REG_LDS;
-                g.T = T;
-                g.EPL = EPL;
-                return;
-            }
+    const int dcm = std::max(1, g.max_dc);
+    // Register-resident messages: at most EPL_REG edges per lane.
+    if (dcm <= EPL_REG) {
+        const int T = std::max(64, round_up64((E + EPL_REG - 1) / EPL_REG));
+        const int EPL = std::max((int)((E + T - 1) / T), dcm);
+        if (T <= 1024 && EPL <= EPL_REG && lds_bytes_for(VAR_REG_LDS, g.n, g.m, T) <= LDS_LIMIT) {
+            g.variant = VAR_REG_LDS;
+            g.T = T;
+            g.EPL = EPL;
+            return;
         }
     }
     // Messages in global scratch: as many lanes as the workgroup allows.
-    int T = (int)std::min<long long>(1024, std::max(64, round_up64((E + 7) / 8)));
-    int EPL = (int)((E + T - 1) / T);
-    while (g.max_dc > EPL && T > 64) {
-        T -= 64;
-        EPL = (int)((E + T - 1) / T);
-    }
+    const int T = (int)std::min<long long>(1024, std::max(64, round_up64((E + 7) / 8)));
     g.T = T;
-    g.EPL = std::max(EPL, 1);
+    g.EPL = std::max((int)((E + T - 1) / T), dcm);
     g.variant = (lds_bytes_for(VAR_GLB_LDS, g.n, g.m, T) <= LDS_LIMIT) ? VAR_GLB_LDS : VAR_GLB_GLB;
 }
 
@@ -299,7 +290,30 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.scratch = w->scratch;
     a.scratch_wg_doubles = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
+#ifdef QL_PHASE_STAMPS
+    const size_t nst = (size_t)wgs * (g->T / 64) * NUM_STAMPS;
+    uint64_t *d_st = nullptr;
+    HIP_TRY(hipMalloc(&d_st, nst * sizeof(uint64_t)));
+    HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
+    a.stamps = d_st;
+#endif
     HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
+#ifdef QL_PHASE_STAMPS
+    {  // diagnostic: per-phase share of wave time, one JSON line on stderr
+        std::vector<uint64_t> h(nst);
+        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipMemcpy(h.data(), d_st, nst * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        (void)hipFree(d_st);
+        double tot[NUM_STAMPS] = {0}, all = 0;
+        for (size_t i = 0; i < nst; ++i) tot[i % NUM_STAMPS] += (double)h[i];
+        for (int i = 0; i < NUM_STAMPS; ++i) all += tot[i];
+        std::string js = "{\"phase_stamps\": {";
+        for (int i = 0; i < NUM_STAMPS; ++i)
+            js += std::string(i ? ", " : "") + "\"" + STAMP_NAMES[i] + "\": " + std::to_string(tot[i] / all);
+        js += "}, \"wave_cycles_total\": " + std::to_string(all) + "}";
+        fprintf(stderr, "%s\n", js.c_str());
+    }
+#endif
     return QLDPC_OK;
 }
 
@@ -565,7 +579,7 @@ int qldpc_keys_match_device(int32_t batch, int32_t n, const uint8_t *d_alice, co
 }
 
 int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream) {
-    if (fn < 0 || fn > 5 || count < 0) return fail(QLDPC_EINVAL, "fn must be 0..5, count >= 0");
+    if (fn < 0 || fn > 7 || count < 0) return fail(QLDPC_EINVAL, "fn must be 0..7, count >= 0");
     if (count > 0 && (!d_in || !d_out)) return fail(QLDPC_EINVAL, "NULL device buffer");
     hipError_t e = launch_math_selftest(fn, count, d_in, d_out, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "math_selftest");

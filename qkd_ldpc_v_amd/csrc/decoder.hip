@@ -175,6 +175,19 @@ struct MetaSrc<0> {
 
 constexpr int CTRL_BYTES = 16;
 
+// Diagnostic build only (-DQL_PHASE_STAMPS): per-wave s_memtime accumulators
+// of every phase's work and barrier-wait time, written to DecodeArgs::stamps.
+#ifdef QL_PHASE_STAMPS
+#define STAMP(id)                                                \
+    do {                                                         \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();        \
+        st_acc[id] += _t - st_last;                              \
+        st_last = _t;                                            \
+    } while (0)
+#else
+#define STAMP(id) ((void)0)
+#endif
+
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Byte layout of the per-frame state block (LDS or global scratch).
@@ -227,9 +240,16 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
     const int head_in = a.lane_head[tid];
     const int row0_in = a.lane_row0[tid];
 
+#ifdef QL_PHASE_STAMPS
+    uint64_t st_acc[NUM_STAMPS];
+    for (int i = 0; i < NUM_STAMPS; ++i) st_acc[i] = 0;
+    uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
         if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        STAMP(ST_SETUP);
         __syncthreads();
+        STAMP(ST_SETUP_WAIT);
         const int f = *s_frame;
         if (f >= a.batch) break;
         const double *llr = a.llr + (size_t)f * n;
@@ -262,7 +282,10 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                     rowflag[j] = (uint8_t)((fl & 5) | (rm << 1));
                     mis |= rm;
                 }
-                if (!__syncthreads_or(mis)) {
+                STAMP(ST_S);
+                const int anymis = __syncthreads_or(mis);
+                STAMP(ST_S_WAIT);
+                if (!anymis) {
                     iters = ADAPT ? it + 1 : it;
                     okv = 1;
                     break;
@@ -295,7 +318,7 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                     if (thr_on) x = clip_msg(x, thr);
                 }
                 if constexpr (SPA_FAM) {
-                    const double t = (ALG == 0) ? ql_exact::tanh_exact(x / 2.) : tanh_lin(x / 2.);
+                    const double t = (ALG == 0) ? ql_exact::tanh_dec(x / 2.) : tanh_lin(x / 2.);
                     c2b.set(k, t);
                     if (k < head) return;
                     if (mt & META_START) acc = ((rowflag[r] & 1) ? -1. : 1.) * t;  // :57-62
@@ -327,7 +350,9 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                     carryI[tid] = ag.neg;
                 }
             }
+            STAMP(ST_CN1);
             __syncthreads();
+            STAMP(ST_CN1_WAIT);
 
             // ---- CN phase 2: finish rows begun in the previous lane ----------------
             if (head > 0) {
@@ -352,7 +377,9 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                     rowflag[row0] = (uint8_t)((rowflag[row0] & 3) | (t.neg << 2));
                 }
             }
+            STAMP(ST_CN2);
             __syncthreads();
+            STAMP(ST_CN2_WAIT);
 
             // ---- CN phase 3: check-to-bit messages, clipped (:64-74 etc.) ---------
             r = row0;
@@ -362,7 +389,7 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                 double c;
                 if constexpr (SPA_FAM) {
                     const double prod = rowA[r] / c2b.get(k);  // :66
-                    c = 2. * ((ALG == 0) ? ql_exact::atanh_exact(prod) : atanh_lin(prod));
+                    c = 2. * ((ALG == 0) ? ql_exact::atanh_dec(prod) : atanh_lin(prod));
                 } else {
                     const double x = c2b.get(k);
                     const uint8_t fl = rowflag[r];
@@ -384,9 +411,12 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                 c2b.set(k, c);
             });
 
+            STAMP(ST_CN3);
             // ---- VN: totals in std::accumulate order (:76-84) -----------------------
             for (int i = tid; i < n; i += T) total[i] = llr[i];
+            STAMP(ST_VN0);
             __syncthreads();
+            STAMP(ST_VN0_WAIT);
             for (int kk = 0; kk < a.dv_max; ++kk) {
                 meta.each(EPL, [&](int k, uint32_t mt) {
                     if ((mt & META_VALID) && ((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
@@ -394,7 +424,9 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                         total[col] = total[col] + c2b.get(k);
                     }
                 });
+                STAMP(ST_VNK);
                 __syncthreads();
+                STAMP(ST_VNK_WAIT);
             }
             had_vn = true;
         }
@@ -411,8 +443,16 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
         }
+        STAMP(ST_OUT);
         __syncthreads();
+        STAMP(ST_OUT_WAIT);
     }
+#ifdef QL_PHASE_STAMPS
+    if ((tid & 63) == 0 && a.stamps) {
+        uint64_t *dst = a.stamps + ((size_t)blockIdx.x * (a.T / 64) + (tid >> 6)) * NUM_STAMPS;
+        for (int i = 0; i < NUM_STAMPS; ++i) dst[i] = st_acc[i];
+    }
+#endif
 }
 
 // ---- QKD_LDPC frame construction (src/qkd_ldpc_algorithm.cpp:1043-1052) --------
@@ -456,7 +496,9 @@ __global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, c
     case 2: y = ql_exact::expm1_exact(x); break;
     case 3: y = ql_exact::log1p_exact(x); break;
     case 4: y = tanh_lin(x); break;
-    default: y = atanh_lin(x); break;
+    case 5: y = atanh_lin(x); break;
+    case 6: y = ql_exact::tanh_dec(x); break;
+    default: y = ql_exact::atanh_dec(x); break;
     }
     out[i] = y;
 }

@@ -26,6 +26,15 @@ enum Variant : int {
     VAR_GLB_GLB = 2,  // everything per-frame in global scratch     (n = 100k)
 };
 
+// Phase ids of the diagnostic stamp build (QL_PHASE_STAMPS).
+enum StampId : int {
+    ST_SETUP, ST_SETUP_WAIT, ST_S, ST_S_WAIT, ST_CN1, ST_CN1_WAIT, ST_CN2, ST_CN2_WAIT, ST_CN3,
+    ST_VN0, ST_VN0_WAIT, ST_VNK, ST_VNK_WAIT, ST_OUT, ST_OUT_WAIT, NUM_STAMPS
+};
+static const char *const STAMP_NAMES[NUM_STAMPS] = {
+    "setup", "setup_wait", "synd", "synd_wait", "cn1", "cn1_wait", "cn2", "cn2_wait", "cn3",
+    "vn_init", "vn_init_wait", "vn_phases", "vn_phases_wait", "out", "out_wait"};
+
 struct DecodeArgs {
     // graph (device pointers; shared by every frame)
     int n, m, E, T, EPL, dv_max, max_dc;
@@ -49,6 +58,7 @@ struct DecodeArgs {
     int *frame_counter;
     double *scratch;              // per-workgroup scratch (variants 1, 2)
     long long scratch_wg_doubles; // doubles per workgroup
+    uint64_t *stamps;             // diagnostic build only: [wg][wave][NUM_STAMPS]
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.

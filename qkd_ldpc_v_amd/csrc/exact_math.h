@@ -251,4 +251,290 @@ QL_HD double atanh_exact(double x) {
     return t;
 }
 
+// ---------------------------------------------------------------------------
+// Branch-free forms (what the GPU kernels call).  Identical IEEE operation
+// sequences to the functions above, but every case's cheap tail is computed and
+// the right one selected, while the expensive shared part (argument reduction,
+// polynomial, the division) runs once.  A wave whose lanes fall in different
+// cases then runs one path instead of several.  Exact for every input
+// (tools/exact_math_check.cpp tests both forms against the C library).
+
+QL_HD double add_exponent(double y, int32_t k) {  // y * 2^k by exponent add (glibc SET_HIGH_WORD)
+    return with_hi_word(y, hi_word(y) + ((uint32_t)k << 20));
+}
+
+QL_HD double expm1_bf(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double Q1 = -3.33333333333331316428e-02, Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05, Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+    const double o_threshold = 7.09782712893383973096e+02;
+
+    const uint32_t hw = hi_word(x);
+    const bool neg = (hw & 0x80000000u) != 0;
+    const uint32_t hx = hw & 0x7fffffffu;
+    // argument reduction: k = 0 (|x| <= ln2/2), +-1 (|x| < 1.5 ln2), else rounded
+    const int32_t kgen = (int32_t)(invln2 * x + (neg ? -0.5 : 0.5));
+    int32_t k = (hx < 0x3FF0A2B2u) ? (neg ? -1 : 1) : kgen;
+    k = (hx > 0x3fd62e42u) ? k : 0;
+    const double t = (double)k;
+    const double hi = x - t * ln2_hi;   // == x - ln2_hi / x + ln2_hi at k = +-1, == x at k = 0
+    const double lo = t * ln2_lo;
+    const double xr = hi - lo;
+    const double c = (hi - xr) - lo;
+    // shared rational correction
+    const double hfx = 0.5 * xr;
+    const double hxs = xr * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t3 = 3.0 - r1 * hfx;
+    const double e = hxs * ((r1 - t3) / (6.0 - xr * t3));
+    // reconstructions
+    const double y0 = xr - (xr * e - hxs);                       // k == 0
+    const double e2 = (xr * (e - c) - c) - hxs;
+    const double ym1 = 0.5 * (xr - e2) - 0.5;                    // k == -1
+    const double yp1 = (xr < -0.25) ? -2.0 * (e2 - (xr + 0.5)) : 1.0 + 2.0 * (xr - e2);  // k == 1
+    const bool far = (k <= -2 || k > 56);
+    const int32_t kb = (k < 2) ? 2 : ((k > 19) ? 19 : k);        // keep the shift defined
+    const double tb = from_words(0x3ff00000u - (0x200000u >> kb), 0u);   // 1 - 2^-k
+    const double tc = from_words((uint32_t)(0x3ff - k) << 20, 0u);       // 2^-k
+    const double ya = (far ? 1.0 : tb) - (e2 - xr);              // far, or 2 <= k < 20
+    const double yc = (xr - (e2 + tc)) + 1.0;                    // 20 <= k <= 56
+    const double ypre = (far || k < 20) ? ya : yc;
+    const double ysc = (k == 1024) ? ypre * 2.0 * 0x1p1023 : add_exponent(ypre, k);
+    double y = far ? ysc - 1.0 : ysc;
+    y = (k == 1) ? yp1 : y;
+    y = (k == -1) ? ym1 : y;
+    y = (k == 0) ? y0 : y;
+    // filters
+    if (hx < 0x3c900000u) y = x;                                 // |x| < 2^-54
+    if (hx >= 0x4043687Au && neg) y = 1.0e-300 - 1.0;            // x < -56 ln2: -1
+    if (hx >= 0x40862E42u) {
+        if (x > o_threshold) y = __builtin_inf();
+        if (hx >= 0x7ff00000u) y = (((hx & 0xfffffu) | lo_word(x)) != 0) ? x + x : (neg ? -1.0 : x);
+    }
+    return y;
+}
+
+QL_HD double log1p_bf(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01;
+    const double Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01;
+    const double Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01;
+    const double Lp7 = 1.479819860511658591e-01;
+
+    const int32_t hx = (int32_t)hi_word(x);
+    const int32_t ax = hx & 0x7fffffff;
+    const bool small = hx < 0x3FDA827A;
+    const bool k0 = small && (hx > 0 || hx <= (int32_t)0xbfd2bec3);  // -0.2929 < x < 0.41422
+    // k != 0 path: u = 1 + x (or x when x >= 2^53), normalised into [sqrt(2)/2, sqrt(2))
+    const bool huge = hx >= 0x43400000;
+    const double u0 = huge ? x : 1.0 + x;
+    int32_t hu = (int32_t)hi_word(u0);
+    int32_t k = (hu >> 20) - 1023;
+    double c = (k > 0) ? 1.0 - (u0 - x) : x - (u0 - 1.0);
+    c = huge ? 0.0 : c / u0;
+    hu &= 0x000fffff;
+    const bool up = hu >= 0x6a09e;
+    const double u = with_hi_word(u0, (uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)));
+    k = up ? k + 1 : k;
+    hu = up ? (0x00100000 - hu) >> 2 : hu;
+    double f = u - 1.0;
+    // k == 0 path takes x itself
+    f = k0 ? x : f;
+    k = k0 ? 0 : k;
+    hu = k0 ? 1 : hu;
+    c = k0 ? 0.0 : c;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    // main series
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double R1 = z * Lp1;
+    const double z2 = z * z;
+    const double R2 = Lp2 + z * Lp3;
+    const double z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5;
+    const double z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    double y = (k == 0) ? f - (hfsq - s * (hfsq + R))
+                        : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    // |f| < 2^-20 path
+    const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+    const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
+    const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+    y = (hu == 0) ? ((f == 0.0) ? yzero : ysmall) : y;
+    // specials
+    if (small && ax < 0x3e200000) y = (ax < 0x3c900000) ? x : x - x * x * 0.5;  // |x| < 2^-29
+    if (small && ax >= 0x3ff00000) y = (x == -1.0) ? -__builtin_inf() : __builtin_nan("");  // x <= -1
+    if (!small && hx >= 0x7ff00000) y = x + x;                                   // +inf / NaN
+    return y;
+}
+
+QL_HD double tanh_bf(double x) {
+    const uint32_t jx = hi_word(x);
+    const uint32_t ix = jx & 0x7fffffffu;
+    const double ax = __builtin_fabs(x);
+    const bool big = ix >= 0x3ff00000u;
+    const double two_ax = 2.0 * ax;
+    const double t = expm1_bf(big ? two_ax : -two_ax);
+    const double q = (big ? 2.0 : -t) / (t + 2.0);
+    double z = big ? 1.0 - q : q;
+    z = (ix >= 0x40360000u) ? 1.0 - 1.0e-300 : z;
+    z = ((int32_t)jx >= 0) ? z : -z;
+    z = (ix < 0x3c800000u) ? x * (1.0 + x) : z;
+    z = (x != x) ? x + x : z;
+    return z;
+}
+
+QL_HD double atanh_bf(double x) {
+    const double xa = __builtin_fabs(x);
+    const bool small = xa < 0.5;
+    const double twoxa = xa + xa;
+    const double qd = (small ? twoxa * xa : twoxa) / (1.0 - xa);
+    double t = 0.5 * log1p_bf(small ? twoxa + qd : qd);
+    t = __builtin_copysign(t, x);
+    t = (xa < 0x1.0p-28) ? x : t;
+    t = (xa > 1.0) ? __builtin_nan("") : t;
+    t = (xa == 1.0) ? __builtin_copysign(__builtin_inf(), x) : t;
+    t = (x != x) ? x + x : t;
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// Decoder forms: tanh / atanh with their expm1 / log1p cores specialised to the
+// arguments tanh and atanh can hand them when their own result is used.
+//   tanh:  the expm1 result matters only for |x| < 22, i.e. for arguments
+//          u in (-2, 0] u [2, 44): k is never 1 or 1024, u is never tiny
+//          (|x| < 2^-55 is tanh's own tiny case), never < -56 ln2, never
+//          overflows.  Those expm1 cases are dropped.
+//   atanh: the log1p result matters only for 2^-28 <= |x| < 1, i.e. for
+//          arguments in [2^-27, 2^54]: finite, >= 0, never tiny.
+// Outside those ranges the final selects of tanh/atanh take over, so both
+// functions remain bit-exact for EVERY input (tools/exact_math_check.cpp).
+
+QL_HD double tanh_dec(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double Q1 = -3.33333333333331316428e-02, Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05, Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+
+    const uint32_t jx = hi_word(x);
+    const uint32_t ix = jx & 0x7fffffffu;
+    const double ax = __builtin_fabs(x);
+    const bool big = ix >= 0x3ff00000u;          // |x| >= 1: expm1(2|x|), else expm1(-2|x|)
+    const double two_ax = 2.0 * ax;
+    const double u = big ? two_ax : -two_ax;
+    // --- expm1(u) core (s_expm1.c) ---
+    const uint32_t uh = hi_word(two_ax);
+    const int32_t kgen = (int32_t)(invln2 * u + (big ? 0.5 : -0.5));
+    int32_t k = (uh < 0x3FF0A2B2u) ? -1 : kgen;  // only u < 0 reaches |u| < 1.5 ln2
+    k = (uh > 0x3fd62e42u) ? k : 0;
+    const double t = (double)k;
+    const double hi = u - t * ln2_hi;
+    const double lo = t * ln2_lo;
+    const double xr = hi - lo;
+    const double c = (hi - xr) - lo;
+    const double hfx = 0.5 * xr;
+    const double hxs = xr * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t3 = 3.0 - r1 * hfx;
+    const double e = hxs * ((r1 - t3) / (6.0 - xr * t3));
+    const double y0 = xr - (xr * e - hxs);                       // k == 0
+    const double e2 = (xr * (e - c) - c) - hxs;
+    const double ym1 = 0.5 * (xr - e2) - 0.5;                    // k == -1
+    const bool far = (k <= -2 || k > 56);
+    const int32_t kb = (k < 2) ? 2 : ((k > 19) ? 19 : k);
+    const double tb = from_words(0x3ff00000u - (0x200000u >> kb), 0u);
+    const double tc = from_words((uint32_t)(0x3ff - k) << 20, 0u);
+    const double ya = (far ? 1.0 : tb) - (e2 - xr);
+    const double yc = (xr - (e2 + tc)) + 1.0;
+    const double ysc = add_exponent((far || k < 20) ? ya : yc, k);
+    double y = far ? ysc - 1.0 : ysc;
+    y = (k == -1) ? ym1 : y;
+    y = (k == 0) ? y0 : y;
+    // --- tanh from t = expm1(u) (s_tanh.c) ---
+    const double q = (big ? 2.0 : -y) / (y + 2.0);
+    double z = big ? 1.0 - q : q;
+    z = (ix >= 0x40360000u) ? 1.0 - 1.0e-300 : z;
+    z = ((int32_t)jx >= 0) ? z : -z;
+    z = (ix < 0x3c800000u) ? x * (1.0 + x) : z;
+    z = (x != x) ? x + x : z;
+    return z;
+}
+
+QL_HD double atanh_dec(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01;
+    const double Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01;
+    const double Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01;
+    const double Lp7 = 1.479819860511658591e-01;
+
+    const double xa = __builtin_fabs(x);
+    const bool smallx = xa < 0.5;
+    const double twoxa = xa + xa;
+    const double qd = (smallx ? twoxa * xa : twoxa) / (1.0 - xa);
+    const double a = smallx ? twoxa + qd : qd;   // log1p argument, in [2^-27, 2^54]
+    // --- log1p(a) core (s_log1p.c) ---
+    const int32_t hx = (int32_t)hi_word(a);
+    const bool k0 = hx < 0x3FDA827A;             // a < 0.41422: f = a, k = 0
+    const bool huge = hx >= 0x43400000;
+    const double u0 = huge ? a : 1.0 + a;
+    int32_t hu = (int32_t)hi_word(u0);
+    int32_t k = (hu >> 20) - 1023;
+    double c = (k > 0) ? 1.0 - (u0 - a) : a - (u0 - 1.0);
+    c = huge ? 0.0 : c / u0;
+    hu &= 0x000fffff;
+    const bool up = hu >= 0x6a09e;
+    const double u = with_hi_word(u0, (uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)));
+    k = up ? k + 1 : k;
+    hu = up ? (0x00100000 - hu) >> 2 : hu;
+    double f = u - 1.0;
+    f = k0 ? a : f;
+    k = k0 ? 0 : k;
+    hu = k0 ? 1 : hu;
+    c = k0 ? 0.0 : c;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double R1 = z * Lp1;
+    const double z2 = z * z;
+    const double R2 = Lp2 + z * Lp3;
+    const double z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5;
+    const double z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    double y = (k == 0) ? f - (hfsq - s * (hfsq + R))
+                        : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+    const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
+    const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+    y = (hu == 0) ? ((f == 0.0) ? yzero : ysmall) : y;
+    // --- atanh (e_atanh.c) ---
+    double t = __builtin_copysign(0.5 * y, x);
+    t = (xa < 0x1.0p-28) ? x : t;
+    t = (xa > 1.0) ? __builtin_nan("") : t;
+    t = (xa == 1.0) ? __builtin_copysign(__builtin_inf(), x) : t;
+    t = (x != x) ? x + x : t;
+    return t;
+}
+
 }  // namespace ql_exact

@@ -69,18 +69,18 @@ def test_device_exact_math_bitwise(gpu_available):
     refs = {0: math.tanh, 2: math.expm1}
     d_in = torch.from_numpy(xs).cuda()
     d_out = torch.empty_like(d_in)
-    for fn, name in ((0, "tanh"), (1, "atanh"), (2, "expm1"), (3, "log1p")):
+    for fn, name in ((0, "tanh"), (1, "atanh"), (2, "expm1"), (3, "log1p"), (6, "tanh_dec"), (7, "atanh_dec")):
         Q._lib.check(Q.lib().qldpc_selftest_math_device(fn, xs.size, d_in.data_ptr(), d_out.data_ptr(), None),
                      "selftest")
         torch.cuda.synchronize()
         got = d_out.cpu().numpy()
-        f = {0: math.tanh, 1: math.atanh, 2: math.expm1, 3: math.log1p}[fn]
+        f = {0: math.tanh, 1: math.atanh, 2: math.expm1, 3: math.log1p, 6: math.tanh, 7: math.atanh}[fn]
 
         def ref(x):
             try:
                 return f(x)
             except (ValueError, OverflowError):
-                if fn == 1:
+                if fn in (1, 7):
                     return math.copysign(math.inf, x) if abs(x) == 1 else math.nan
                 if fn == 3:
                     return -math.inf if x == -1 else math.nan

@@ -39,8 +39,8 @@ int main(int argc, char **argv) {
     long per = argc > 1 ? atol(argv[1]) : 1000000;
     uint64_t seed0 = argc > 2 ? strtoull(argv[2], 0, 10) : 12345;
     unsigned nt = std::thread::hardware_concurrency(); if (!nt) nt = 4;
-    const char *names[4] = {"tanh", "atanh", "expm1", "log1p"};
-    std::atomic<long> bad[4]; for (auto &b : bad) b = 0;
+    const char *names[10] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec"};
+    std::atomic<long> bad[10]; for (auto &b : bad) b = 0;
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] {
         uint64_t s = seed0 * 1000003 + t;
@@ -53,11 +53,17 @@ int main(int argc, char **argv) {
             double z = (mode == 1) ? x * 1.5 : x;
             if (!same(ql_exact::expm1_exact(z), std::expm1(z))) { if (bad[2]++ < 5) printf("expm1 x=%a got=%a ref=%a\n", z, ql_exact::expm1_exact(z), std::expm1(z)); }
             if (!same(ql_exact::log1p_exact(x), std::log1p(x))) { if (bad[3]++ < 5) printf("log1p x=%a got=%a ref=%a\n", x, ql_exact::log1p_exact(x), std::log1p(x)); }
+            if (!same(ql_exact::tanh_bf(x), std::tanh(x))) { if (bad[4]++ < 5) printf("tanh_bf  x=%a got=%a ref=%a\n", x, ql_exact::tanh_bf(x), std::tanh(x)); }
+            if (!same(ql_exact::atanh_bf(y), std::atanh(y))) { if (bad[5]++ < 5) printf("atanh_bf x=%a got=%a ref=%a\n", y, ql_exact::atanh_bf(y), std::atanh(y)); }
+            if (!same(ql_exact::expm1_bf(z), std::expm1(z))) { if (bad[6]++ < 5) printf("expm1_bf x=%a got=%a ref=%a\n", z, ql_exact::expm1_bf(z), std::expm1(z)); }
+            if (!same(ql_exact::tanh_dec(x), std::tanh(x))) { if (bad[8]++ < 5) printf("tanh_dec  x=%a got=%a ref=%a\n", x, ql_exact::tanh_dec(x), std::tanh(x)); }
+            if (!same(ql_exact::atanh_dec(y), std::atanh(y))) { if (bad[9]++ < 5) printf("atanh_dec x=%a got=%a ref=%a\n", y, ql_exact::atanh_dec(y), std::atanh(y)); }
+            if (!same(ql_exact::log1p_bf(x), std::log1p(x))) { if (bad[7]++ < 5) printf("log1p_bf x=%a got=%a ref=%a\n", x, ql_exact::log1p_bf(x), std::log1p(x)); }
         }
     });
     for (auto &x : th) x.join();
     long tot = 0;
-    for (int f = 0; f < 4; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
+    for (int f = 0; f < 10; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
     // Sweep the high words around every branch boundary of the four functions.
     const uint32_t bounds[] = {0x3FDA827A, 0xbfd2bec3, 0xbfd2bec4, 0x3e200000, 0x3c900000, 0x43400000, 0x3ff00000,
                                0x3fd62e42, 0x3FF0A2B2, 0x4043687A, 0x40862E42, 0x40360000, 0x3c800000, 0x3fe00000,
@@ -70,10 +76,14 @@ int main(int argc, char **argv) {
                     const uint32_t hi = (base + d) ^ (sg ? 0x80000000u : 0u);
                     const uint64_t b = ((uint64_t)hi << 32) | lo;
                     double x; memcpy(&x, &b, 8);
-                    const double r[4] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x)};
-                    const double g[4] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
-                                         ql_exact::log1p_exact(x)};
-                    for (int f = 0; f < 4; ++f) {
+                    const double r[10] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
+                                         std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
+                                         std::tanh(x), std::atanh(x)};
+                    const double g[10] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
+                                         ql_exact::log1p_exact(x), ql_exact::tanh_bf(x), ql_exact::atanh_bf(x),
+                                         ql_exact::expm1_bf(x), ql_exact::log1p_bf(x), ql_exact::tanh_dec(x),
+                                         ql_exact::atanh_dec(x)};
+                    for (int f = 0; f < 10; ++f) {
                         ++nb;
                         if (!same(r[f], g[f]) && bb++ < 5) printf("boundary %s x=%a ref=%a got=%a\n", names[f], x, r[f], g[f]);
                     }
