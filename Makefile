@@ -11,7 +11,10 @@ HOSTCHK := $(PKG)/host/host_mirror_check
 
 all: $(LIB) $(ORACLE) $(HOSTCHK)
 
-$(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+$(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
@@ -20,17 +23,17 @@ $(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include
 $(CSRC)/loaders.o: $(CSRC)/loaders.cpp $(CSRC)/loaders.hpp
 	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(LIB): $(CSRC)/decoder.o $(CSRC)/capi.o $(CSRC)/loaders.o
+$(LIB): $(CSRC)/decoder.o $(CSRC)/decoder_v2.o $(CSRC)/capi.o $(CSRC)/loaders.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
 # Diagnostic build with per-phase s_memtime stamps (never the product).
 STAMPLIB := $(PKG)/diag/libqkdldpc_hip.so
 stamps: $(STAMPLIB)
-$(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+$(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
-$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
+$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
 	mkdir -p $(PKG)/diag
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 

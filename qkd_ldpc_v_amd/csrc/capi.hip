@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -51,6 +52,10 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     int *counter = nullptr;
     double *scratch = nullptr;
     size_t scratch_doubles = 0;
+    // V2 frame format (palette + 2-bit codes), capacity in frames
+    uint8_t *codes = nullptr, *pal_ok = nullptr;
+    double *palette = nullptr;
+    size_t code_frames = 0;
 };
 
 struct HostIO {  // device staging buffers of the host-buffer entry
@@ -66,6 +71,7 @@ struct DeviceGraph {
     int num_cus = 0;
     uint32_t *slot_meta = nullptr;
     int32_t *lane_row0 = nullptr, *lane_head = nullptr, *ell_col = nullptr, *row_deg = nullptr;
+    int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
     HostIO io;
@@ -76,6 +82,8 @@ struct DeviceGraph {
 
 struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
+    int v2R = 0, n_iso = 0;                 // V2: register slots per lane, bits of degree 0
+    std::vector<int> wave_rows;             // V2: first row of each wave (+ m)
     std::vector<std::unique_ptr<DeviceGraph>> devs;
 };
 
@@ -85,8 +93,18 @@ const char *variant_name(int v) {
     switch (v) {
     case VAR_REG_LDS: return "reg_lds";
     case VAR_GLB_LDS: return "glb_lds";
+    case VAR_V2: return "v2";
     default: return "glb_glb";
     }
+}
+
+size_t lds_of(const qldpc_graph &g, int alg) {
+    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m) : lds_bytes_for(g.variant, g.n, g.m, g.T);
+}
+
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
 }
 
 int round_up64(long long x) { return (int)(((x + 63) / 64) * 64); }
@@ -112,6 +130,54 @@ void plan(qldpc_graph &g) {
     g.T = T;
     g.EPL = std::max((int)((E + T - 1) / T), dcm);
     g.variant = (lds_bytes_for(VAR_GLB_LDS, g.n, g.m, T) <= LDS_LIMIT) ? VAR_GLB_LDS : VAR_GLB_GLB;
+}
+
+// V2 plan: rows dealt to W waves in contiguous blocks balanced by edge count,
+// each wave's edges dealt EPL_w per lane to its 64 lanes (EPL_w >= max_dc keeps
+// a row within two adjacent lanes of ONE wave).  W is the fewest waves whose
+// lanes do not need more than max_dc slots (more would only add idle waves
+// and barrier cost), capped by the instantiation's workgroup size; R is the
+// smallest register-slot instantiation that holds the plan.  QLDPC_V2_WAVES
+// forces W.  Returns false when no V2 instantiation fits (v1 is used).
+bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
+    if (g.max_dc <= 0) return false;
+    for (int j = 0; j < g.m; ++j)
+        if (row_ptr[j + 1] == row_ptr[j]) return false;  // empty rows: v1 checks them by row-ELL
+    if (lds_bytes_v2(2, g.n, g.m) > LDS_LIMIT) return false;
+    const long long E = g.E;
+    const int forced = env_int("QLDPC_V2_WAVES", 0);
+    for (int R : {V2_R_SMALL, V2_R_MID}) {
+        const int wmax = v2_threads_for(R) / 64;
+        int W = forced > 0 ? forced : (int)std::min<long long>(wmax, (E + 64LL * g.max_dc - 1) / (64LL * g.max_dc));
+        W = std::max(1, W);
+        if (W > wmax) continue;
+        std::vector<int> rb(W + 1, g.m);
+        rb[0] = 0;
+        for (int w = 1; w < W; ++w) {
+            const long long target = E * w / W;
+            int j = rb[w - 1];
+            while (j < g.m && row_ptr[j + 1] <= target) ++j;  // rows ending at or before target
+            if (j < g.m && target - row_ptr[j] > row_ptr[j + 1] - target) ++j;  // nearer boundary
+            rb[w] = j;
+        }
+        int epl = 0;
+        bool ok = true;
+        for (int w = 0; w < W && ok; ++w) {
+            const long long ew = row_ptr[rb[w + 1]] - row_ptr[rb[w]];
+            if (ew == 0) continue;
+            const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
+            ok = e <= R;
+            epl = std::max(epl, e);
+        }
+        if (!ok) continue;
+        g.variant = VAR_V2;
+        g.v2R = R;
+        g.T = W * 64;
+        g.EPL = epl;
+        g.wave_rows = rb;
+        return true;
+    }
+    return false;
 }
 
 template <typename T>
@@ -152,8 +218,17 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     }
     for (int i = 0; i < n; ++i) g->dv_max = std::max(g->dv_max, dv[i]);
     if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 64");
-    plan(*g);
+    // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
+    const char *want = std::getenv("QLDPC_VARIANT");
+    const bool v1_only = want && std::strcmp(want, "v1") == 0;
+    if (v1_only || !plan_v2(*g, row_ptr)) plan(*g);
+    if (want && std::strcmp(want, "v2") == 0 && g->variant != VAR_V2)
+        return fail(QLDPC_EUNSUP, "QLDPC_VARIANT=v2 but no V2 instantiation holds this graph");
     const int T = g->T, EPL = g->EPL;
+    std::vector<int32_t> iso;
+    for (int i = 0; i < n; ++i)
+        if (dv[i] == 0) iso.push_back(i);
+    g->n_iso = (int)iso.size();
 
     // Lane partition metadata.
     std::vector<int> row_of(E), kpos(E), seen(n, 0);
@@ -162,32 +237,42 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             row_of[e] = j;
             kpos[e] = seen[col_idx[e]]++;
         }
-    // uint4 groups per lane, group-major [g][lane][4]; the register variant
-    // always has EPL_REG/4 groups at lane stride REG_TSTRIDE.
-    const bool reg = g->variant == VAR_REG_LDS;
-    const int G4 = reg ? EPL_REG / 4 : (EPL + 3) / 4;
+    // uint4 groups per lane, group-major [g][lane][4]; the register variants
+    // have a fixed group count at lane stride REG_TSTRIDE.
+    const bool v2 = g->variant == VAR_V2;
+    const bool reg = g->variant == VAR_REG_LDS || v2;
+    const int G4 = v2 ? g->v2R / 4 : (reg ? EPL_REG / 4 : (EPL + 3) / 4);
     const int TS = reg ? REG_TSTRIDE : T;
     std::vector<uint32_t> meta((size_t)G4 * TS * 4, 0);
     std::vector<int32_t> lrow0(T, -1), lhead(T, 0);
-    for (int l = 0; l < T; ++l) {
-        const long long e0 = (long long)l * EPL;
-        if (e0 < E) {
-            const int r0 = row_of[e0];
-            lrow0[l] = r0;
-            if (e0 != row_ptr[r0]) lhead[l] = row_ptr[r0 + 1] - (int)e0;
-        }
-        int prev_row = -1;
-        for (int k = 0; k < EPL; ++k) {
-            const long long e = e0 + k;
-            if (e >= E) break;
-            const int j = row_of[e];
-            uint32_t w = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
-            if (e == row_ptr[j]) w |= META_START;
-            if (e == row_ptr[j + 1] - 1) w |= META_END;
-            if (k > 0 && j != prev_row && j != prev_row + 1)
-                return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
-            prev_row = j;
-            meta[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = w;
+    // Lane l holds edges [e_begin, e_end) of its wave (v1: one "wave" of T lanes).
+    const int W = v2 ? T / 64 : 1;
+    for (int w = 0; w < W; ++w) {
+        const long long wb = v2 ? row_ptr[g->wave_rows[w]] : 0;
+        const long long we = v2 ? row_ptr[g->wave_rows[w + 1]] : E;
+        const int lanes = v2 ? 64 : T;
+        const int epl_w = v2 ? std::max<int>((int)((we - wb + 63) / 64), g->max_dc) : EPL;
+        for (int li = 0; li < lanes; ++li) {
+            const int l = w * 64 + li;
+            const long long e0 = wb + (long long)li * epl_w;
+            if (e0 < we) {
+                const int r0 = row_of[e0];
+                lrow0[l] = r0;
+                if (e0 != row_ptr[r0]) lhead[l] = row_ptr[r0 + 1] - (int)e0;
+            }
+            int prev_row = -1;
+            for (int k = 0; k < epl_w; ++k) {
+                const long long e = e0 + k;
+                if (e >= we) break;
+                const int j = row_of[e];
+                uint32_t wd = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
+                if (e == row_ptr[j]) wd |= META_START;
+                if (e == row_ptr[j + 1] - 1) wd |= META_END;
+                if (k > 0 && j != prev_row && j != prev_row + 1)
+                    return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
+                prev_row = j;
+                meta[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = wd;
+            }
         }
     }
     // Row-ELL (slot-major) for syndrome evaluation.
@@ -222,7 +307,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         int rc;
         if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->ell_col, ell)) ||
-            (rc = upload(&dg->row_deg, rdeg))) {
+            (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso))) {
             (void)hipSetDevice(prev);
             return rc;
         }
@@ -247,36 +332,66 @@ int check_params(const qldpc_params *p) {
     return QLDPC_OK;
 }
 
-// Enqueue the decoder for `batch` device-resident frames on `stream`.
+// Per-stream workspace of a device graph, created on first use.
+Workspace *workspace(DeviceGraph *dg, hipStream_t stream) { return &dg->ws[(void *)stream]; }
+
+// Ensure the workspace holds V2 frame codes for `batch` frames (caller holds dg->mu).
+int ensure_codes(qldpc_graph *g, Workspace *w, int batch, hipStream_t stream) {
+    if ((size_t)batch <= w->code_frames) return QLDPC_OK;
+    HIP_TRY(hipStreamSynchronize(stream));
+    (void)hipFree(w->codes);
+    (void)hipFree(w->palette);
+    (void)hipFree(w->pal_ok);
+    w->codes = nullptr; w->palette = nullptr; w->pal_ok = nullptr; w->code_frames = 0;
+    const size_t nc = (size_t)(g->n + 3) / 4;
+    HIP_TRY(hipMalloc(&w->codes, (size_t)batch * nc));
+    HIP_TRY(hipMalloc(&w->palette, (size_t)batch * 4 * sizeof(double)));
+    HIP_TRY(hipMalloc(&w->pal_ok, (size_t)batch));
+    w->code_frames = (size_t)batch;
+    return QLDPC_OK;
+}
+
+// Enqueue the decoder for `batch` device-resident frames on `stream`.  For the
+// V2 kernel the frames' palette + codes are taken from the stream's workspace
+// when `codes_ready` (written by build_frames), else computed here from llr.
 int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch, const double *llr,
               const uint8_t *synd, uint8_t *bits, uint32_t *iters, uint8_t *ok, double *post,
-              hipStream_t stream) {
+              hipStream_t stream, bool codes_ready = false) {
     if (batch == 0) return QLDPC_OK;
     const int alg = p->algorithm;
-    const size_t lds = lds_bytes_for(g->variant, g->n, g->m, g->T);
+    const bool v2 = g->variant == VAR_V2;
+    const size_t lds = lds_of(*g, alg);
     Workspace *w;
     int wgs;
     {
         std::lock_guard<std::mutex> lk(dg->mu);
         if (dg->occ[alg] == 0) {
             int b = 0;
-            HIP_TRY(occupancy(g->variant, alg, g->T, lds, &b));
+            if (v2) HIP_TRY(occupancy_v2(g->v2R, alg, g->T, lds, &b));
+            else HIP_TRY(occupancy(g->variant, alg, g->T, lds, &b));
             if (b <= 0) return fail(QLDPC_EUNSUP, "decoder kernel cannot be resident with this graph shape");
             dg->occ[alg] = b;
         }
         wgs = std::min(batch, dg->occ[alg] * dg->num_cus);
-        w = &dg->ws[(void *)stream];
+        w = workspace(dg, stream);
         if (!w->counter) HIP_TRY(hipMalloc(&w->counter, 64));
-        const long long per = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
-        const size_t need = (size_t)per * (size_t)wgs;
-        if (need > w->scratch_doubles) {
-            if (w->scratch) {
-                HIP_TRY(hipStreamSynchronize(stream));
-                HIP_TRY(hipFree(w->scratch));
-                w->scratch = nullptr;
+        if (v2) {
+            if (codes_ready && (size_t)batch > w->code_frames)
+                return fail(QLDPC_EINVAL, "frame codes were not built for this batch");
+            int rc = ensure_codes(g, w, batch, stream);
+            if (rc) return rc;
+        } else {
+            const long long per = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+            const size_t need = (size_t)per * (size_t)wgs;
+            if (need > w->scratch_doubles) {
+                if (w->scratch) {
+                    HIP_TRY(hipStreamSynchronize(stream));
+                    HIP_TRY(hipFree(w->scratch));
+                    w->scratch = nullptr;
+                }
+                HIP_TRY(hipMalloc(&w->scratch, need * sizeof(double)));
+                w->scratch_doubles = need;
             }
-            HIP_TRY(hipMalloc(&w->scratch, need * sizeof(double)));
-            w->scratch_doubles = need;
         }
     }
     DecodeArgs a{};
@@ -288,7 +403,12 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
     a.frame_counter = w->counter;
     a.scratch = w->scratch;
-    a.scratch_wg_doubles = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.scratch_wg_doubles = v2 ? 0 : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.nc = (g->n + 3) / 4;
+    a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
+    a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R;
+    if (v2 && !codes_ready)
+        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
 #ifdef QL_PHASE_STAMPS
     const size_t nst = (size_t)wgs * (g->T / 64) * NUM_STAMPS;
@@ -297,7 +417,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
     a.stamps = d_st;
 #endif
-    HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
+    if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
+    else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
 #ifdef QL_PHASE_STAMPS
     {  // diagnostic: per-phase share of wave time, one JSON line on stderr
         std::vector<uint64_t> h(nst);
@@ -309,7 +430,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         for (int i = 0; i < NUM_STAMPS; ++i) all += tot[i];
         std::string js = "{\"phase_stamps\": {";
         for (int i = 0; i < NUM_STAMPS; ++i)
-            js += std::string(i ? ", " : "") + "\"" + STAMP_NAMES[i] + "\": " + std::to_string(tot[i] / all);
+            js += std::string(i ? ", " : "") + "\"" + STAMP_NAMES[i] + "\": " + std::to_string(all > 0 ? tot[i] / all : 0.);
         js += "}, \"wave_cycles_total\": " + std::to_string(all) + "}";
         fprintf(stderr, "%s\n", js.c_str());
     }
@@ -412,9 +533,13 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->lane_head);
         (void)hipFree(d->ell_col);
         (void)hipFree(d->row_deg);
+        (void)hipFree(d->iso_bits);
         for (auto &kv : d->ws) {
             (void)hipFree(kv.second.counter);
             (void)hipFree(kv.second.scratch);
+            (void)hipFree(kv.second.codes);
+            (void)hipFree(kv.second.palette);
+            (void)hipFree(kv.second.pal_ok);
         }
         HostIO &io = d->io;
         (void)hipFree(io.llr); (void)hipFree(io.post); (void)hipFree(io.synd); (void)hipFree(io.bits); (void)hipFree(io.ok); (void)hipFree(io.iters);
@@ -439,7 +564,7 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
     if (algorithm < 0 || algorithm > 5) return fail(QLDPC_EINVAL, "algorithm must be 0..5");
     DeviceGraph *dg = find_dev(const_cast<qldpc_graph *>(g), device);
     if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
-    const size_t lds = lds_bytes_for(g->variant, g->n, g->m, g->T);
+    const size_t lds = lds_of(*g, algorithm);
     if (lanes) *lanes = g->T;
     if (edges_per_lane) *edges_per_lane = g->EPL;
     if (lds_bytes) *lds_bytes = (int32_t)lds;
@@ -449,7 +574,8 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
         HIP_TRY(hipGetDevice(&prev));
         HIP_TRY(hipSetDevice(dg->device));
         int b = 0;
-        hipError_t e = occupancy(g->variant, algorithm, g->T, lds, &b);
+        hipError_t e = g->variant == VAR_V2 ? occupancy_v2(g->v2R, algorithm, g->T, lds, &b)
+                                            : occupancy(g->variant, algorithm, g->T, lds, &b);
         (void)hipSetDevice(prev);
         if (e != hipSuccess) return hip_fail(e, "occupancy");
         *workgroups = b * dg->num_cus;
@@ -563,7 +689,7 @@ int qldpc_build_frames_device(qldpc_graph *g, int32_t device, int32_t batch, con
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
     hipError_t e = launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob,
-                                       d_log_p, d_llr, d_syndrome, (hipStream_t)stream);
+                                       d_log_p, d_llr, d_syndrome, nullptr, nullptr, nullptr, (hipStream_t)stream);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return hip_fail(e, "build_frames");
     return QLDPC_OK;
@@ -590,16 +716,41 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
                                 const uint8_t *d_alice, const uint8_t *d_bob, const double *d_log_p,
                                 double *d_llr_ws, uint8_t *d_synd_ws, uint8_t *d_bits_out, uint32_t *d_iters_out,
                                 uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out, void *stream) {
-    int rc = qldpc_build_frames_device(g, device, batch, d_alice, d_bob, d_log_p, d_llr_ws, d_synd_ws, stream);
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    int rc = check_params(p);
     if (rc) return rc;
-    rc = qldpc_decode_batch_device(g, device, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out,
-                                   nullptr, stream);
-    if (rc) return rc;
-    if (!d_keys_match_out) return QLDPC_OK;
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch > 0 && (!d_alice || !d_bob || !d_log_p || !d_llr_ws || !d_synd_ws || !d_bits_out || !d_iters_out ||
+                      !d_synd_ok_out))
+        return fail(QLDPC_EINVAL, "NULL device buffer");
+    DeviceGraph *dg = find_dev(g, device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    if (batch == 0) return QLDPC_OK;
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
-    rc = qldpc_keys_match_device(batch, g->n, d_alice, d_bits_out, d_keys_match_out, stream);
+    const hipStream_t s = (hipStream_t)stream;
+    auto body = [&]() -> int {
+        // The frame builder writes the V2 palette + codes straight into the
+        // stream's workspace, so the decoder skips the palettize pass.
+        uint8_t *codes = nullptr, *pal_ok = nullptr;
+        double *palette = nullptr;
+        if (g->variant == VAR_V2) {
+            std::lock_guard<std::mutex> lk(dg->mu);
+            Workspace *w = workspace(dg, s);
+            int r = ensure_codes(g, w, batch, s);
+            if (r) return r;
+            codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
+        }
+        HIP_TRY(launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob, d_log_p,
+                                    d_llr_ws, d_synd_ws, codes, palette, pal_ok, s));
+        int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
+                          g->variant == VAR_V2);
+        if (r) return r;
+        if (d_keys_match_out) HIP_TRY(launch_keys_match(batch, g->n, d_alice, d_bits_out, d_keys_match_out, s));
+        return QLDPC_OK;
+    };
+    rc = body();
     (void)hipSetDevice(prev);
     return rc;
 }

@@ -24,7 +24,15 @@ enum Variant : int {
     VAR_REG_LDS = 0,  // messages in VGPRs, totals/rows in LDS       (n <~ 14k)
     VAR_GLB_LDS = 1,  // messages in per-workgroup global scratch, totals/rows in LDS
     VAR_GLB_GLB = 2,  // everything per-frame in global scratch     (n = 100k)
+    VAR_V2 = 3,       // wave-aligned register kernel (decoder_v2.hip)
 };
+
+// Register slots per lane of the V2 instantiations.  (A third, 84 slots x 8
+// waves, holds no more edges than 56 x 12 and its SPA build falls back to a
+// scratch array, so it is not built.)
+constexpr int V2_R_SMALL = 44, V2_R_MID = 56;
+// Workgroup size each V2 instantiation is compiled for (its VGPR budget).
+constexpr __host__ __device__ int v2_threads_for(int R) { return R <= V2_R_SMALL ? 1024 : 768; }
 
 // Phase ids of the diagnostic stamp build (QL_PHASE_STAMPS).
 enum StampId : int {
@@ -59,6 +67,14 @@ struct DecodeArgs {
     double *scratch;              // per-workgroup scratch (variants 1, 2)
     long long scratch_wg_doubles; // doubles per workgroup
     uint64_t *stamps;             // diagnostic build only: [wg][wave][NUM_STAMPS]
+    // V2 frame format: channel LLRs as a 4-entry palette + 2-bit codes
+    int nc;                  // code bytes per frame = ceil(n / 4)
+    const uint8_t *codes;    // [batch][nc]
+    const double *palette;   // [batch][4]
+    const uint8_t *pal_ok;   // [batch]; 0 -> the decoder gathers llr[] instead
+    int n_iso;               // bits with no check (dv = 0): total = llr
+    const int32_t *iso_bits; // [n_iso]
+    int v2R;                 // register slots of the V2 instantiation to launch
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -73,7 +89,14 @@ hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_
 
 hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
                                int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
-                               double *llr, uint8_t *synd, hipStream_t stream);
+                               double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
+                               hipStream_t stream);
+
+size_t lds_bytes_v2(int alg, int n, int m);
+hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
+hipError_t occupancy_v2(int R, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
+hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
+                            uint8_t *pal_ok, hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
                              uint8_t *match, hipStream_t stream);

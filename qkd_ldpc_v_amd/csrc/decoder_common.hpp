@@ -1,0 +1,153 @@
+// decoder_common.hpp — device helpers shared by the decoder kernels.
+#pragma once
+#include <float.h>
+
+#include "decoder.hpp"
+#include "exact_math.h"
+
+namespace qldpc {
+namespace dev {
+
+// threshold_matrix (src/array_and_matrix_operations.cpp:953-972): NaN passes.
+__device__ __forceinline__ double clip_msg(double v, double thr) {
+    if (v > thr) return thr;
+    if (v < -thr) return -thr;
+    return v;
+}
+
+// tanh_lin_approx / atanh_lin_approx (src/qkd_ldpc_algorithm.cpp:146-172).
+__device__ __forceinline__ double tanh_lin(double x) {
+    const double a = fabs(x);
+    double r;
+    if (a < 0.5) r = 0.9242 * a;
+    else if (a < 0.9) r = 0.6355 * a + 0.1444;
+    else if (a < 1.2) r = 0.3912 * a + 0.3642;
+    else if (a < 1.75) r = 0.1958 * a + 0.5986;
+    else if (a < 2.5) r = 0.0603 * a + 0.8358;
+    else if (a < 3.5) r = 0.0115 * a + 0.9577;
+    else if (a < 8) r = 0.0004 * a + 0.9967;
+    else r = 1;
+    return (x < 0.) ? -r : r;
+}
+__device__ __forceinline__ double atanh_lin(double x) {
+    const double a = fabs(x);
+    double r;
+    if (a < 0.7) r = 1.196 * a - 0.0323;
+    else if (a < 0.9) r = 2.9187 * a - 1.214;
+    else if (a < 0.999) r = 10.8717 * a - 8.3717;
+    else r = 2510.9 * a - 2505.9;
+    return (x < 0.) ? -r : r;
+}
+
+// Min-sum row aggregate: parity of x<0, and the two smallest |x| with the
+// reference's strict-< scan (src/qkd_ldpc_algorithm.cpp:381-397).  The scan's
+// result is the two smallest of {|x| : |x| < DBL_MAX} padded with DBL_MAX, so
+// partial aggregates merge order-free (exact).
+struct MinAgg {
+    double m1, m2;
+    int neg;
+};
+__device__ __forceinline__ void agg_init(MinAgg &a) {
+    a.m1 = DBL_MAX;
+    a.m2 = DBL_MAX;
+    a.neg = 0;
+}
+__device__ __forceinline__ void agg_push(MinAgg &a, double x) {
+    if (x < 0) a.neg ^= 1;
+    const double ax = fabs(x);
+    if (ax < a.m1) {
+        a.m2 = a.m1;
+        a.m1 = ax;
+    } else if (ax < a.m2) {
+        a.m2 = ax;
+    }
+}
+__device__ __forceinline__ void agg_merge(MinAgg &a, const MinAgg &b) {
+    a.neg ^= b.neg;
+    const bool bl = b.m1 < a.m1;
+    const double lo = bl ? b.m1 : a.m1;
+    const double hi = bl ? a.m1 : b.m1;
+    const double m2 = (a.m2 < b.m2) ? a.m2 : b.m2;
+    a.m1 = lo;
+    a.m2 = (hi < m2) ? hi : m2;
+}
+
+// Per-edge message storage of one lane.
+template <int R>
+struct EdgeMsgs {  // VGPR-resident: R slots, indexed only by unrolled constants
+    double v[R];
+    __device__ __forceinline__ void bind(double *, int, int) {}
+    __device__ __forceinline__ double get(int k) const { return v[k]; }
+    __device__ __forceinline__ void set(int k, double x) { v[k] = x; }
+};
+template <>
+struct EdgeMsgs<0> {  // per-workgroup global scratch, slot-major [k][lane]: coalesced
+    double *p;
+    int T;
+    __device__ __forceinline__ void bind(double *base, int tid, int TT) {
+        p = base + tid;
+        T = TT;
+    }
+    __device__ __forceinline__ double get(int k) const { return p[(size_t)k * T]; }
+    __device__ __forceinline__ void set(int k, double x) { p[(size_t)k * T] = x; }
+};
+
+// Visit this lane's slots in order, handing each slot's metadata word to f.
+// Metadata is one uint4 per four consecutive slots, group-major [g][lane], so a
+// wave reads 1 KiB contiguous per group.  The register variant uses a fixed
+// group stride of REG_TSTRIDE lanes and buffer loads whose group offset is a
+// compile-time constant: no per-group address stays live across the kernel.
+#ifdef QL_SLOT_FENCE
+#define QL_SLOT_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define QL_SLOT_BARRIER() ((void)0)
+#endif
+
+template <int R>
+struct MetaSrc {
+    __amdgpu_buffer_rsrc_t rs;
+    int voff;
+    __device__ __forceinline__ void init(const uint32_t *base, int tid, int) {
+        rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (R / 4) * REG_TSTRIDE * 16, 0x00020000);
+        voff = tid * 16;
+    }
+    template <typename F>
+    __device__ __forceinline__ void each(int, F &&f) const {
+        static_assert(R % 4 == 0, "register slots come in groups of four");
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, g * REG_TSTRIDE * 16, 0);
+            f(4 * g + 0, (uint32_t)q[0]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 1, (uint32_t)q[1]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 2, (uint32_t)q[2]);
+            QL_SLOT_BARRIER();
+            f(4 * g + 3, (uint32_t)q[3]);
+            QL_SLOT_BARRIER();
+        }
+    }
+};
+template <>
+struct MetaSrc<0> {
+    const uint4 *mp;
+    int T;
+    __device__ __forceinline__ void init(const uint32_t *base, int tid, int TT) {
+        mp = reinterpret_cast<const uint4 *>(base) + tid;
+        T = TT;
+    }
+    template <typename F>
+    __device__ __forceinline__ void each(int EPL, F &&f) const {
+        const int G = (EPL + 3) >> 2;
+        for (int g = 0; g < G; ++g) {
+            const uint4 q = mp[(size_t)g * T];
+            f(4 * g + 0, q.x);
+            f(4 * g + 1, q.y);
+            f(4 * g + 2, q.z);
+            f(4 * g + 3, q.w);
+        }
+    }
+};
+
+}  // namespace dev
+}  // namespace qldpc

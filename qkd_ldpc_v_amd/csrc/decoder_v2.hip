@@ -1,0 +1,381 @@
+// decoder_v2.hip — wave-aligned register decoder (variant V2) for gfx950.
+//
+// Same decoders and bit-exactness contract as decoder.hip (reference
+// src/qkd_ldpc_algorithm.cpp:3-1029), restructured to cut barriers:
+//   * rows are dealt to WAVES (contiguous blocks, balanced by edges), then a
+//     wave's edges to its 64 lanes, EPL per lane (<= R, compile-time register
+//     slots).  A row may straddle two lanes of one wave, never two waves, so a
+//     split row's running product / min-sum aggregate / parity moves by one
+//     wave shuffle instead of an LDS round trip and two barriers;
+//   * the syndrome check (reference :86,101-107 and :745-776) is fused into the
+//     check-node pass, which gathers every total[col] anyway: each row's
+//     parity of the current hard decision is folded into the row scan;
+//   * VN phase 0 (total = llr + first message) is fused into the message
+//     pass; the channel LLRs live in LDS as a 4-entry palette + 2-bit codes
+//     (every frame the reference builds has <= 4 distinct LLRs: +-log_p, 1e-4,
+//     DBL_MAX); frames that do not fit gather llr[] from global instead.
+// Per iteration: 1 barrier after the check-node scan, 1 after the message
+// pass, 1 per remaining VN phase (dv_max - 1).
+#include "decoder_common.hpp"
+
+namespace qldpc {
+
+namespace {
+
+using namespace dev;
+
+constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
+
+__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+struct V2Layout {
+    size_t total, rowA, rowB, rowflag, codes, palette, bytes;
+    __host__ __device__ V2Layout(int n, int m, int nc, bool minsum) {
+        size_t o = V2_CTRL;
+        total = o; o = al16(o + (size_t)n * 8);
+        rowA = o; o = al16(o + (size_t)m * 8);
+        rowB = o; o = al16(o + (minsum ? (size_t)m * 8 : 0));
+        palette = o; o = al16(o + 4 * 8);
+        rowflag = o; o = al16(o + (size_t)m);
+        codes = o; o = al16(o + (size_t)nc);
+        bytes = o;
+    }
+};
+
+// Threads per workgroup each instantiation is built for: 16 waves at 44 slots
+// (128 VGPRs), 12 waves at 56 (168).
+template <int R>
+constexpr int v2_max_threads() { return v2_threads_for(R); }
+
+template <int ALG, int R>
+__global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
+    constexpr bool ADAPT = (ALG == 4 || ALG == 5);
+    constexpr bool NORM = (ALG == 2 || ALG == 4);
+
+    const int tid = threadIdx.x;
+    const int T = a.T, n = a.n, m = a.m, nc = a.nc;
+    const double thr = a.thr;
+    const bool thr_on = a.thr_on != 0;
+    const V2Layout L(n, m, nc, !SPA_FAM);
+    int *s_frame = reinterpret_cast<int *>(smem);
+    int *s_flag = reinterpret_cast<int *>(smem) + 1;
+    double *total = reinterpret_cast<double *>(smem + L.total);
+    double *rowA = reinterpret_cast<double *>(smem + L.rowA);
+    double *rowB = reinterpret_cast<double *>(smem + L.rowB);
+    double *pal = reinterpret_cast<double *>(smem + L.palette);
+    uint8_t *rowflag = smem + L.rowflag;  // bit0 target syndrome, bit1 row mismatch, bit2 neg parity
+    uint8_t *codes = smem + L.codes;
+
+    EdgeMsgs<R> c2b;
+    MetaSrc<R> meta;
+    meta.init(a.slot_meta, tid, T);
+    const int head_in = a.lane_head[tid];
+    const int row0_in = a.lane_row0[tid];
+    int epoch = 0;
+    if (tid == 0) *s_flag = 0;
+
+    for (;;) {
+        if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        __syncthreads();
+        const int f = *s_frame;
+        if (f >= a.batch) break;
+        const uint8_t *sy = a.synd + (size_t)f * m;
+        for (int j = tid; j < m; j += T) rowflag[j] = sy[j] & 1;
+        const bool paletted = a.pal_ok[f] != 0;
+        const double *gllr = a.llr ? a.llr + (size_t)f * n : nullptr;
+        {
+            const uint8_t *cs = a.codes + (size_t)f * nc;
+            for (int i = tid; i < nc; i += T) codes[i] = cs[i];
+            if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
+            if constexpr (ADAPT)
+                for (int i = tid; i < n; i += T) total[i] = 0.0;  // total_bit_llr starts zeroed
+        }
+        __syncthreads();
+        auto llr_of = [&](int col) -> double {
+            if (paletted) return pal[(codes[col >> 2] >> ((col & 3) * 2)) & 3];
+            return gllr[col];
+        };
+
+        int iters = a.max_it, okv = 0;
+        bool had_vn = false;
+        for (int it = 0;; ++it) {
+            const bool check = ADAPT ? (it < a.max_it) : (it > 0);
+            const bool compute = it < a.max_it;
+            ++epoch;
+            int head = head_in, row0 = row0_in;
+            asm volatile("" : "+v"(head), "+v"(row0));
+
+            // ---- check-node scan: b2c, tanh / aggregates, row parity of z ----
+            int r = row0;
+            double acc = 0.0;
+            MinAgg ag, hag;
+            agg_init(ag);
+            agg_init(hag);
+            int par = 0, hpar = 0;
+            bool tail_open = false;
+            meta.each(0, [&](int k, uint32_t mt) {
+                if (!(mt & META_VALID)) return;
+                const bool start = (mt & META_START) != 0;
+                if (k > 0 && start) ++r;
+                const int col = (int)(mt & META_COL_MASK);
+                const double tv = had_vn ? total[col] : llr_of(col);
+                const int zb = (tv <= 0.0) ? 1 : 0;
+                double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
+                if (had_vn) {
+                    x = tv - c2b.get(k);  // (:115)
+                    if (thr_on) x = clip_msg(x, thr);
+                }
+                double t = x;
+                if constexpr (SPA_FAM) {
+                    if (compute) t = (ALG == 0) ? ql_exact::tanh_dec(x / 2.) : tanh_lin(x / 2.);
+                }
+                c2b.set(k, t);
+                if (k < head) {  // tail of a row begun in the previous lane
+                    hpar ^= zb;
+                    if constexpr (!SPA_FAM) agg_push(hag, x);
+                    return;
+                }
+                if (start) {
+                    par = 0;
+                    if constexpr (!SPA_FAM) agg_init(ag);
+                }
+                par ^= zb;
+                if constexpr (SPA_FAM) {
+                    if (start) acc = ((rowflag[r] & 1) ? -1. : 1.) * t;  // (:57-62)
+                    else acc = acc * t;
+                } else {
+                    agg_push(ag, x);
+                }
+                if (mt & META_END) {
+                    const int fl = rowflag[r];
+                    const int mis = (par ^ fl) & 1;
+                    if constexpr (SPA_FAM) {
+                        rowA[r] = acc;
+                        rowflag[r] = (uint8_t)((fl & 1) | (mis << 1));
+                    } else {
+                        rowA[r] = ag.m1;
+                        rowB[r] = ag.m2;
+                        rowflag[r] = (uint8_t)((fl & 1) | (mis << 1) | (ag.neg << 2));
+                    }
+                    if (mis) *s_flag = epoch;
+                }
+                tail_open = !(mt & META_END);
+            });
+            // ---- rows split across two lanes of this wave: one shuffle ----
+            {
+                const int lane = tid & 63;
+                const int up = (lane == 0) ? 0 : lane - 1;
+                const int ppar = __shfl(tail_open ? par : 0, up, 64);
+                if constexpr (SPA_FAM) {
+                    const double pacc = __shfl(acc, up, 64);
+                    if (head > 0) {
+                        double p = pacc;
+                        if constexpr (R > 0) {
+#pragma unroll
+                            for (int k = 0; k < R; ++k)
+                                if (k < head) p = p * c2b.get(k);
+                        }
+                        const int fl = rowflag[row0];
+                        const int mis = (ppar ^ hpar ^ fl) & 1;
+                        rowA[row0] = p;
+                        rowflag[row0] = (uint8_t)((fl & 1) | (mis << 1));
+                        if (mis) *s_flag = epoch;
+                    }
+                } else {
+                    MinAgg t;
+                    t.m1 = __shfl(ag.m1, up, 64);
+                    t.m2 = __shfl(ag.m2, up, 64);
+                    t.neg = __shfl(ag.neg, up, 64);
+                    if (head > 0) {
+                        agg_merge(t, hag);
+                        const int fl = rowflag[row0];
+                        const int mis = (ppar ^ hpar ^ fl) & 1;
+                        rowA[row0] = t.m1;
+                        rowB[row0] = t.m2;
+                        rowflag[row0] = (uint8_t)((fl & 1) | (mis << 1) | (t.neg << 2));
+                        if (mis) *s_flag = epoch;
+                    }
+                }
+            }
+            __syncthreads();
+            const bool anymis = *s_flag == epoch;
+            if (check && !anymis) {
+                iters = ADAPT ? it + 1 : it;
+                okv = 1;
+                break;
+            }
+            if (!compute) break;
+
+            // ---- check-to-bit messages + VN phase 0 (total = llr + first message) ----
+            r = row0;
+            meta.each(0, [&](int k, uint32_t mt) {
+                if (!(mt & META_VALID)) return;
+                if (k > 0 && (mt & META_START)) ++r;
+                double c;
+                if constexpr (SPA_FAM) {
+                    const double prod = rowA[r] / c2b.get(k);  // :66
+                    c = 2. * ((ALG == 0) ? ql_exact::atanh_dec(prod) : atanh_lin(prod));
+                } else {
+                    const double x = c2b.get(k);
+                    const int fl = rowflag[r];
+                    double sp = (fl & 1) ? -1. : 1.;                   // :376
+                    sp *= ((fl >> 2) & 1) ? -1. : 1.;                  // :398
+                    const double prod = sp * ((x > 0) ? 1. : -1.);     // :402
+                    const double m1 = rowA[r];
+                    const double sel = (fabs(x) == m1) ? rowB[r] : m1; // :406
+                    double fac = a.primary;
+                    if (ADAPT && (fl & 2)) fac = a.secondary;          // :749-757
+                    if constexpr (NORM) {
+                        c = fac * prod * sel;
+                    } else {
+                        const double d = sel - fac;
+                        c = prod * ((d < 0.) ? 0. : d);
+                    }
+                }
+                if (thr_on) c = clip_msg(c, thr);
+                c2b.set(k, c);
+                if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == 0) {
+                    const int col = (int)(mt & META_COL_MASK);
+                    total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
+                }
+            });
+            __syncthreads();
+            // ---- remaining VN phases: the k-th message of every bit, in check order ----
+            for (int kk = 1; kk < a.dv_max; ++kk) {
+                meta.each(0, [&](int k, uint32_t mt) {
+                    if ((mt & META_VALID) && ((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
+                        const int col = (int)(mt & META_COL_MASK);
+                        total[col] = total[col] + c2b.get(k);
+                    }
+                });
+                __syncthreads();
+            }
+            had_vn = true;
+        }
+
+        // ---- outputs ----
+        if (had_vn)
+            for (int q = tid; q < a.n_iso; q += T) total[a.iso_bits[q]] = llr_of(a.iso_bits[q]);  // dv = 0
+        __syncthreads();
+        uint8_t *bits = a.bits + (size_t)f * n;
+        double *post = a.post ? a.post + (size_t)f * n : nullptr;
+        for (int i = tid; i < n; i += T) {
+            const double z = had_vn ? total[i] : llr_of(i);
+            bits[i] = (z <= 0.0) ? 1 : 0;
+            if (post) post[i] = total[i];
+        }
+        if (tid == 0) {
+            a.iters[f] = (uint32_t)iters;
+            a.ok[f] = (uint8_t)okv;
+        }
+        __syncthreads();
+    }
+}
+
+// Palette + 2-bit codes of each frame's LLRs (one workgroup per frame).  Wave 0
+// collects up to 4 distinct values (bitwise) in first-occurrence order; a frame
+// with more gets pal_ok = 0 and the decoder gathers its llr[] instead.
+__global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const double *llr, uint8_t *codes,
+                                                        double *palette, uint8_t *pal_ok) {
+    __shared__ unsigned long long pv[4];
+    __shared__ int pcount, over;
+    const size_t f = blockIdx.x;
+    const unsigned long long *v = reinterpret_cast<const unsigned long long *>(llr + f * (size_t)n);
+    if (threadIdx.x < 64) {
+        int cnt = 0;
+        unsigned long long p[4] = {0, 0, 0, 0};
+        bool overflow = false;
+        for (int base = 0; base < n && !overflow; base += 64) {
+            const int i = base + threadIdx.x;
+            const unsigned long long x = (i < n) ? v[i] : p[0];
+            bool known = (i >= n);
+            for (int q = 0; q < 4; ++q) known |= (q < cnt) && (x == p[q]);
+            unsigned long long pending = __ballot(!known);
+            while (pending) {
+                if (cnt == 4) { overflow = true; break; }
+                const int src = __builtin_ctzll(pending);
+                const unsigned long long nv = __shfl(x, src, 64);
+                p[cnt++] = nv;
+                known |= (x == nv);
+                pending = __ballot(!known);
+            }
+        }
+        if (threadIdx.x == 0) {
+            for (int q = 0; q < 4; ++q) pv[q] = p[q];
+            pcount = cnt;
+            over = overflow ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    const int cnt = pcount;
+    if (threadIdx.x < 4) palette[f * 4 + threadIdx.x] = __builtin_bit_cast(double, pv[threadIdx.x]);
+    if (threadIdx.x == 0) pal_ok[f] = over ? 0 : 1;
+    uint8_t *cs = codes + f * (size_t)nc;
+    for (int j = threadIdx.x; j < nc; j += blockDim.x) {
+        int byte = 0;
+        for (int s = 0; s < 4; ++s) {
+            const int i = 4 * j + s;
+            int code = 0;
+            if (i < n)
+                for (int q = 1; q < 4; ++q)
+                    if (q < cnt && v[i] == pv[q]) code = q;
+            byte |= code << (2 * s);
+        }
+        cs[j] = (uint8_t)byte;
+    }
+}
+
+using KernelFn = void (*)(DecodeArgs);
+
+template <int R>
+KernelFn pick_v2(int alg) {
+    switch (alg) {
+    case 0: return decode_v2_kernel<0, R>;
+    case 1: return decode_v2_kernel<1, R>;
+    case 2: return decode_v2_kernel<2, R>;
+    case 3: return decode_v2_kernel<3, R>;
+    case 4: return decode_v2_kernel<4, R>;
+    default: return decode_v2_kernel<5, R>;
+    }
+}
+
+KernelFn kernel_v2(int R, int alg) {
+    switch (R) {
+    case V2_R_SMALL: return pick_v2<V2_R_SMALL>(alg);
+    default: return pick_v2<V2_R_MID>(alg);
+    }
+}
+
+}  // namespace
+
+size_t lds_bytes_v2(int alg, int n, int m) {
+    return V2Layout(n, m, (n + 3) / 4, alg >= 2).bytes;
+}
+
+hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
+    KernelFn k = kernel_v2(a.v2R, a.alg);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(workgroups), dim3(a.T), lds_bytes, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t occupancy_v2(int R, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
+    KernelFn k = kernel_v2(R, alg);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, T, lds_bytes);
+}
+
+hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
+                            uint8_t *pal_ok, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(palettize_kernel, dim3(batch), dim3(256), 0, stream, n, nc, llr, codes, palette, pal_ok);
+    return hipGetLastError();
+}
+
+}  // namespace qldpc

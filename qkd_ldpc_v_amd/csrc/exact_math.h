@@ -522,12 +522,16 @@ QL_HD double atanh_dec(double x) {
     const double z6 = z4 * z2;
     const double R4 = Lp6 + z * Lp7;
     const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
-    double y = (k == 0) ? f - (hfsq - s * (hfsq + R))
-                        : dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
-    const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
-    const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
-    const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
-    y = (hu == 0) ? ((f == 0.0) ? yzero : ysmall) : y;
+    // k == 0 uses the k != 0 formula with dk = c = 0: 0*ln2_hi - ((hfsq - (P + 0)) - f)
+    // == f - (hfsq - P) bitwise, since a - b == -(b - a) exactly and no zero
+    // result occurs on this path (f = a > 0).
+    double y = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    if (__builtin_expect(hu == 0, 0)) {          // |f| < 2^-20: rare
+        const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+        const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
+        const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+        y = (f == 0.0) ? yzero : ysmall;
+    }
     // --- atanh (e_atanh.c) ---
     double t = __builtin_copysign(0.5 * y, x);
     t = (xa < 0x1.0p-28) ? x : t;

@@ -22,10 +22,23 @@ ALGS = [  # (alg, primary, secondary) — NOPT_R=0,82 / config-map style factors
 _graphs = {}
 
 
-def graph(name):
-    if name not in _graphs:
-        _graphs[name] = Q.Graph(load_fixture(name))
-    return _graphs[name]
+def graph(name, variant="auto"):
+    """Device graph of a fixture; variant "v1" forces the first-generation
+    planner (QLDPC_VARIANT is read when the graph is created)."""
+    import os
+
+    key = (name, variant)
+    if key not in _graphs:
+        old = os.environ.pop("QLDPC_VARIANT", None)
+        if variant != "auto":
+            os.environ["QLDPC_VARIANT"] = variant
+        try:
+            _graphs[key] = Q.Graph(load_fixture(name))
+        finally:
+            os.environ.pop("QLDPC_VARIANT", None)
+            if old is not None:
+                os.environ["QLDPC_VARIANT"] = old
+    return _graphs[key]
 
 
 def frames(H, qber, batch, seed):
@@ -36,11 +49,11 @@ def frames(H, qber, batch, seed):
 
 
 def assert_parity(name, alg, prim, sec, qber, batch, max_it=50, thr_on=True, thr=100.0, seed=0, threads=16,
-                  llr=None, synd=None):
+                  llr=None, synd=None, variant="auto"):
     H = load_fixture(name)
     if llr is None:
         _, _, llr, synd = frames(H, qber, batch, seed)
-    g = graph(name)
+    g = graph(name, variant)
     out = g.decode(Q.Params(alg, max_it, thr_on, thr, prim, sec), llr, synd, posterior=True)
     O = Oracle(H)
     ob, oi, ok, op = O.decode_batch(O.params(alg, max_it, thr_on, thr, prim, sec), llr, synd, threads=threads,
@@ -103,15 +116,56 @@ def test_kat_johnson_on_gpu(gpu_available):
     assert bits_equal_nan(out.posterior[0], np.array(E["posterior_iteration_1"]))
 
 
+def test_planner_picks_wave_aligned_kernel(gpu_available):
+    for name in ("c1_n1024_m220.alist", "c2_n10240_m2201.alist", "c3_n10240_m1801.alist"):
+        for alg, _, _ in ALGS:
+            assert graph(name).plan(0, alg)["variant"] == "v2", name
+        assert graph(name, "v1").plan(0, Q.SPA)["variant"] == "reg_lds", name
+
+
+@pytest.mark.parametrize("variant", ["auto", "v1"])
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-def test_c1_1k_all_algorithms(gpu_available, alg, prim, sec):
+def test_c1_1k_all_algorithms(gpu_available, alg, prim, sec, variant):
     # QBER above the code's threshold region: a mix of converging and failing frames
-    assert_parity("c1_n1024_m220.alist", alg, prim, sec, qber=0.03, batch=96, seed=alg)
+    assert_parity("c1_n1024_m220.alist", alg, prim, sec, qber=0.03, batch=96, seed=alg, variant=variant)
+
+
+@pytest.mark.parametrize("variant", ["auto", "v1"])
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_c2_10k_all_algorithms(gpu_available, alg, prim, sec, variant):
+    assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.026, batch=24, seed=10 + alg, variant=variant)
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-def test_c2_10k_all_algorithms(gpu_available, alg, prim, sec):
-    out, _ = assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.026, batch=24, seed=10 + alg)
+def test_c2_unpaletted_llrs(gpu_available, alg, prim, sec):
+    """Frames with more than 4 distinct LLR values (soft channel inputs): the V2
+    kernel gathers llr[] from HBM instead of the LDS palette."""
+    H = load_fixture("c2_n10240_m2201.alist")
+    a, b, llr, s = frames(H, 0.024, 16, 70 + alg)
+    rng = np.random.default_rng(71 + alg)
+    llr = llr * rng.uniform(0.6, 1.4, llr.shape)
+    llr[::2, :5] = [1e-4, -1e-4, 0.0, -0.0, DBL_MAX]  # specials in half the frames
+    assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0, batch=16, llr=llr, synd=s)
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_c2_rate_adapted_palette(gpu_available, alg, prim, sec):
+    """Punctured (1e-4) and shortened (DBL_MAX) positions on the V2 kernel: four
+    distinct LLRs per frame, i.e. a full palette."""
+    H = load_fixture("c2_n10240_m2201.alist")
+    rng = np.random.default_rng(80 + alg)
+    a, b, llr, s = frames(H, 0.02, 12, 81 + alg)
+    pos = rng.permutation(H.n)
+    punct, short = pos[:300], pos[300:500]
+    a[:, short] = 0
+    b[:, short] = 0
+    s = H.syndrome(a)
+    lp = Q.log_p(0.02)
+    llr = np.where(b != 0, -lp, lp)
+    llr[:, punct] = 1e-4
+    llr[:, short] = DBL_MAX
+    for thr_on in (True, False):
+        assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0, batch=12, thr_on=thr_on, llr=llr, synd=s)
 
 
 def test_c2_spa_headline_config(gpu_available):
@@ -140,6 +194,7 @@ def test_c4_100k_all_global_variant(gpu_available, alg, prim, sec):
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_iteration_cap_edges(gpu_available, alg, prim, sec, max_it):
     assert_parity("c1_n1024_m220.alist", alg, prim, sec, qber=0.02, batch=32, max_it=max_it, seed=7)
+    assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.024, batch=8, max_it=max_it, seed=17)
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
