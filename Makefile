@@ -43,8 +43,13 @@ $(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h
 $(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -I include $< -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/..' -o $@
 
+# FP64 VALU ceilings of the SPA edge math (tools/valu_bench.hip), run on the box.
+tools/valu_bench: tools/valu_bench.hip $(CSRC)/exact_math.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off $< -o $@
+valu_bench: tools/valu_bench
+
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK) $(STAMPLIB)
+	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK) $(STAMPLIB) tools/valu_bench
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean stamps
+.PHONY: all clean stamps valu_bench

@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="frames per GPU (default: the workload's)")
     ap.add_argument("--max-iterations", type=int, default=50)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the steps alternate over: step i+1's frames start on CUs freed by "
+                         "step i's last frames (1 = strictly serial steps)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -86,35 +89,44 @@ def main():
     ta = torch.from_numpy(a).to(dev)
     tb = torch.from_numpy(b).to(dev)
     tlp = torch.full((batch,), lp, dtype=torch.float64, device=dev)
-    llr_ws = torch.empty((batch, n), dtype=torch.float64, device=dev)
-    syn_ws = torch.empty((batch, m), dtype=torch.uint8, device=dev)
-    bits = torch.empty((batch, n), dtype=torch.uint8, device=dev)
-    iters = torch.empty(batch, dtype=torch.int32, device=dev)
-    ok = torch.empty(batch, dtype=torch.uint8, device=dev)
-    km = torch.empty(batch, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    nst = max(1, args.streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
+
+    class Slot:  # per-stream frame workspace and outputs
+        def __init__(self, s):
+            self.stream = s
+            self.llr_ws = torch.empty((batch, n), dtype=torch.float64, device=dev)
+            self.syn_ws = torch.empty((batch, m), dtype=torch.uint8, device=dev)
+            self.bits = torch.empty((batch, n), dtype=torch.uint8, device=dev)
+            self.iters = torch.empty(batch, dtype=torch.int32, device=dev)
+            self.ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+            self.km = torch.empty(batch, dtype=torch.uint8, device=dev)
+
+    slots = [Slot(s) for s in streams]
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
-    def step(i=None):
-        g.build_frames_device(ta, tb, tlp, llr_ws, syn_ws, stream=stream)
-        if i is not None:
-            ev0[i].record(stream)
-        g.decode_device(params, llr_ws, syn_ws, bits, iters, ok, stream=stream)
-        if i is not None:
-            ev1[i].record(stream)
-        Q.keys_match_device(ta, bits, km, stream=stream)
+    def step(i, timed=False):
+        sl = slots[i % nst]
+        st = sl.stream
+        g.build_frames_device(ta, tb, tlp, sl.llr_ws, sl.syn_ws, stream=st)
+        if timed:
+            ev0[i].record(st)
+        g.decode_device(params, sl.llr_ws, sl.syn_ws, sl.bits, sl.iters, sl.ok, stream=st)
+        if timed:
+            ev1[i].record(st)
+        Q.keys_match_device(ta, sl.bits, sl.km, stream=st)
 
     log(f"[rank {rank}] {desc}; plan {plan}; warmup {args.warmup}")
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, timed=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -122,9 +134,10 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([ev0[i].elapsed_time(ev1[i]) for i in range(args.steps)]))
 
-    it_sum = int(iters.to(torch.int64).sum().item())
-    n_ok = int(ok.to(torch.int64).sum().item())
-    n_keys = int(km.to(torch.int64).sum().item())
+    last = slots[(args.steps - 1) % nst]  # every step decodes the same trials
+    it_sum = int(last.iters.to(torch.int64).sum().item())
+    n_ok = int(last.ok.to(torch.int64).sum().item())
+    n_keys = int(last.km.to(torch.int64).sum().item())
     stats = torch.tensor([elapsed, it_sum, n_ok, n_keys, batch, kernel_ms], dtype=torch.float64, device=dev)
     if dist:
         mx = stats.clone()
@@ -165,7 +178,7 @@ def main():
                 "algorithm": Q.ALGORITHM_NAMES[alg], "qber": qber, "max_iterations": args.max_iterations,
                 "batch_per_gpu": batch, "global_batch": int(frames_step),
                 "parallelism": f"frames sharded over {world} GPU(s), no collectives",
-                "kernel_variant": plan["variant"], "lanes_per_frame": plan["lanes"],
+                "kernel_variant": plan["variant"], "lanes_per_frame": plan["lanes"], "streams": nst,
                 "edges_per_lane": plan["edges_per_lane"], "workgroups": plan["workgroups"],
             },
             "fer": 1.0 - ok_total / frames_step,

@@ -84,19 +84,25 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const uint8_t *sy = a.synd + (size_t)f * m;
         for (int j = tid; j < m; j += T) rowflag[j] = sy[j] & 1;
         const bool paletted = a.pal_ok[f] != 0;
-        const double *gllr = a.llr ? a.llr + (size_t)f * n : nullptr;
+        // Non-paletted frames gather llr[] through a buffer resource: a distinct
+        // load kind the compiler cannot fuse with the LDS palette read into a
+        // flat load.
+        const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.llr + (size_t)f * n), (short)0, paletted ? 0 : n * 8, 0x00020000);
         {
             const uint8_t *cs = a.codes + (size_t)f * nc;
             for (int i = tid; i < nc; i += T) codes[i] = cs[i];
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
-            if constexpr (ADAPT)
-                for (int i = tid; i < n; i += T) total[i] = 0.0;  // total_bit_llr starts zeroed
         }
         __syncthreads();
         auto llr_of = [&](int col) -> double {
             if (paletted) return pal[(codes[col >> 2] >> ((col & 3) * 2)) & 3];
-            return gllr[col];
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
         };
+        // total starts as the channel LLRs: the check-node scan of iteration 0
+        // reads the channel decision from it, and bits of degree 0 keep it.
+        for (int i = tid; i < n; i += T) total[i] = llr_of(i);
+        __syncthreads();
 
         int iters = a.max_it, okv = 0;
         bool had_vn = false;
@@ -120,7 +126,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const bool start = (mt & META_START) != 0;
                 if (k > 0 && start) ++r;
                 const int col = (int)(mt & META_COL_MASK);
-                const double tv = had_vn ? total[col] : llr_of(col);
+                const double tv = total[col];
                 const int zb = (tv <= 0.0) ? 1 : 0;
                 double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
                 if (had_vn) {
@@ -256,15 +262,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         }
 
         // ---- outputs ----
-        if (had_vn)
-            for (int q = tid; q < a.n_iso; q += T) total[a.iso_bits[q]] = llr_of(a.iso_bits[q]);  // dv = 0
-        __syncthreads();
+        // ANMSA/AOMSA's total_bit_llr starts zeroed (:738): posterior 0 when the
+        // channel decision already satisfied the syndrome.
+        const bool zero_post = ADAPT && !had_vn;
         uint8_t *bits = a.bits + (size_t)f * n;
         double *post = a.post ? a.post + (size_t)f * n : nullptr;
         for (int i = tid; i < n; i += T) {
-            const double z = had_vn ? total[i] : llr_of(i);
+            const double z = total[i];
             bits[i] = (z <= 0.0) ? 1 : 0;
-            if (post) post[i] = total[i];
+            if (post) post[i] = zero_post ? 0.0 : z;
         }
         if (tid == 0) {
             a.iters[f] = (uint32_t)iters;

@@ -13,7 +13,8 @@
 // (tools/exact_math_check.cpp), hundreds of millions of inputs per function.
 //
 // Rules for this file: every operation is a plain IEEE-754 binary64 op (no FMA
-// contraction: compile with -ffp-contract=off), divisions are true divisions,
+// contraction: compile with -ffp-contract=off), divisions are true divisions
+// (or div_rn_safe where the operands provably need no scaling: same bits),
 // and the evaluation order below is load-bearing.  Branches are written as
 // branches; the compiler turns short ones into selects.
 #pragma once
@@ -39,6 +40,28 @@ QL_HD double with_hi_word(double x, uint32_t hi) {
     b = (b & 0xffffffffull) | ((uint64_t)hi << 32);
     return __builtin_bit_cast(double, b);
 }
+// a / b for operands the caller has proven to lie in the range where gfx950's
+// IEEE division sequence applies no scaling (both |a|, |b| in [2^-900, 2^900]
+// or a == 0, quotient normal, b finite non-zero).  There v_div_scale_f64
+// returns its operands unchanged, v_div_fmas_f64 is a plain fma and
+// v_div_fixup_f64 passes the quotient through, so dropping those three leaves
+// the identical Newton-Raphson + correction sequence: the same correctly
+// rounded quotient in 8 instructions instead of 11.  The host divides.
+QL_HD double div_rn_safe(double a, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = a * r;
+    const double rem = __builtin_fma(-b, q, a);
+    return __builtin_fma(rem, r, q);
+#else
+    return a / b;
+#endif
+}
+
 QL_HD double from_words(uint32_t hi, uint32_t lo) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint64_t)lo);
 }
@@ -454,7 +477,8 @@ QL_HD double tanh_dec(double x) {
     const double R3 = Q4 + hxs * Q5;
     const double r1 = R1 + h2 * R2 + h4 * R3;
     const double t3 = 3.0 - r1 * hfx;
-    const double e = hxs * ((r1 - t3) / (6.0 - xr * t3));
+    // |xr| <= 0.35: denominator ~6, numerator ~-2 (div_rn_safe range)
+    const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
     const double y0 = xr - (xr * e - hxs);                       // k == 0
     const double e2 = (xr * (e - c) - c) - hxs;
     const double ym1 = 0.5 * (xr - e2) - 0.5;                    // k == -1
@@ -469,7 +493,8 @@ QL_HD double tanh_dec(double x) {
     y = (k == -1) ? ym1 : y;
     y = (k == 0) ? y0 : y;
     // --- tanh from t = expm1(u) (s_tanh.c) ---
-    const double q = (big ? 2.0 : -y) / (y + 2.0);
+    // used only for 2^-55 <= |x| < 22: y + 2 in [1.13, 1.3e19], q in [1.5e-19, 0.87]
+    const double q = div_rn_safe(big ? 2.0 : -y, y + 2.0);
     double z = big ? 1.0 - q : q;
     z = (ix >= 0x40360000u) ? 1.0 - 1.0e-300 : z;
     z = ((int32_t)jx >= 0) ? z : -z;
@@ -489,7 +514,8 @@ QL_HD double atanh_dec(double x) {
     const double xa = __builtin_fabs(x);
     const bool smallx = xa < 0.5;
     const double twoxa = xa + xa;
-    const double qd = (smallx ? twoxa * xa : twoxa) / (1.0 - xa);
+    // result used only for 2^-28 <= |x| < 1: numerator in [2^-55, 2), 1 - |x| in [2^-53, 1]
+    const double qd = div_rn_safe(smallx ? twoxa * xa : twoxa, 1.0 - xa);
     const double a = smallx ? twoxa + qd : qd;   // log1p argument, in [2^-27, 2^54]
     // --- log1p(a) core (s_log1p.c) ---
     const int32_t hx = (int32_t)hi_word(a);
@@ -499,7 +525,8 @@ QL_HD double atanh_dec(double x) {
     int32_t hu = (int32_t)hi_word(u0);
     int32_t k = (hu >> 20) - 1023;
     double c = (k > 0) ? 1.0 - (u0 - a) : a - (u0 - 1.0);
-    c = huge ? 0.0 : c / u0;
+    // matters only for a in [0.414, 2^54): c = 0 or |c| in [2^-54, 2], u0 in [1.4, 2^54]
+    c = huge ? 0.0 : div_rn_safe(c, u0);
     hu &= 0x000fffff;
     const bool up = hu >= 0x6a09e;
     const double u = with_hi_word(u0, (uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)));
@@ -512,7 +539,7 @@ QL_HD double atanh_dec(double x) {
     c = k0 ? 0.0 : c;
     const double hfsq = 0.5 * f * f;
     const double dk = (double)k;
-    const double s = f / (2.0 + f);
+    const double s = div_rn_safe(f, 2.0 + f);       // f = 0 or |f| in [2^-54, 0.42]
     const double z = s * s;
     const double R1 = z * Lp1;
     const double z2 = z * z;
