@@ -84,7 +84,7 @@ def main():
     params = Q.Params(alg, args.max_iterations, True, 100.0, prim, sec)
 
     # ---- trials (not timed): synthetic BSC keys, resident in HBM ----
-    a, b, q_acc = Q.bsc_frames(n, qber, batch, seed=1022025 + 7919 * rank)
+    a, b, q_acc = Q.bsc_frames(n, qber, batch, seed=rank_seed(rank))
     lp = Q.log_p(q_acc)
     ta = torch.from_numpy(a).to(dev)
     tb = torch.from_numpy(b).to(dev)
@@ -138,15 +138,9 @@ def main():
     it_sum = int(last.iters.to(torch.int64).sum().item())
     n_ok = int(last.ok.to(torch.int64).sum().item())
     n_keys = int(last.km.to(torch.int64).sum().item())
-    stats = torch.tensor([elapsed, it_sum, n_ok, n_keys, batch, kernel_ms], dtype=torch.float64, device=dev)
-    if dist:
-        mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
-        elapsed_max, kernel_ms_max = float(mx[0]), float(mx[5])
-    else:
-        elapsed_max, kernel_ms_max = elapsed, kernel_ms
-    it_total, ok_total, keys_total, frames_step = (float(stats[1]), float(stats[2]), float(stats[3]), float(stats[4]))
+    tot = combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, batch, kernel_ms, dev)
+    elapsed_max, kernel_ms_max = tot["elapsed_max"], tot["kernel_ms_max"]
+    it_total, ok_total, keys_total, frames_step = tot["iters"], tot["ok"], tot["keys"], tot["frames"]
 
     if rank == 0:
         frames_total = frames_step * args.steps
@@ -204,6 +198,26 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def rank_seed(rank: int) -> int:
+    """Trial seed of a rank: every rank decodes its own, disjoint synthetic frames."""
+    return 1022025 + 7919 * rank
+
+
+def combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, frames, kernel_ms, device):
+    """Max over ranks of the timed region, sums of the per-rank counters: the
+    only collectives of the run, after the timed region (no data-path
+    exchange; frames are independent)."""
+    import torch
+
+    stats = torch.tensor([elapsed, it_sum, n_ok, n_keys, frames, kernel_ms], dtype=torch.float64, device=device)
+    mx = stats.clone()
+    if dist is not None:
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+    return {"elapsed_max": float(mx[0]), "kernel_ms_max": float(mx[5]), "iters": float(stats[1]),
+            "ok": float(stats[2]), "keys": float(stats[3]), "frames": float(stats[4])}
 
 
 def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info):
