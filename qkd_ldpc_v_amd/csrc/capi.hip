@@ -71,6 +71,7 @@ struct DeviceGraph {
     int num_cus = 0;
     uint32_t *slot_meta = nullptr;
     int32_t *lane_row0 = nullptr, *lane_head = nullptr, *ell_col = nullptr, *row_deg = nullptr;
+    int32_t *lane_nst = nullptr, *lane_epl = nullptr;
     int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
@@ -99,7 +100,7 @@ const char *variant_name(int v) {
 }
 
 size_t lds_of(const qldpc_graph &g, int alg) {
-    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m) : lds_bytes_for(g.variant, g.n, g.m, g.T);
+    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T) : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
 int env_int(const char *name, int dflt) {
@@ -140,10 +141,10 @@ void plan(qldpc_graph &g) {
 // smallest register-slot instantiation that holds the plan.  QLDPC_V2_WAVES
 // forces W.  Returns false when no V2 instantiation fits (v1 is used).
 bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
-    if (g.max_dc <= 0) return false;
+    // head <= 31 (tail parity in a 32-bit mask), dummy column id n < 2^20
+    if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
     for (int j = 0; j < g.m; ++j)
         if (row_ptr[j + 1] == row_ptr[j]) return false;  // empty rows: v1 checks them by row-ELL
-    if (lds_bytes_v2(2, g.n, g.m) > LDS_LIMIT) return false;
     const long long E = g.E;
     const int forced = env_int("QLDPC_V2_WAVES", 0);
     for (int R : {V2_R_SMALL, V2_R_MID}) {
@@ -151,6 +152,7 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         int W = forced > 0 ? forced : (int)std::min<long long>(wmax, (E + 64LL * g.max_dc - 1) / (64LL * g.max_dc));
         W = std::max(1, W);
         if (W > wmax) continue;
+        if (lds_bytes_v2(2, g.n, g.m, W * 64) > LDS_LIMIT) continue;
         std::vector<int> rb(W + 1, g.m);
         rb[0] = 0;
         for (int w = 1; w < W; ++w) {
@@ -168,6 +170,14 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
             const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
             ok = e <= R;
             epl = std::max(epl, e);
+            // rows started per lane must fit the 32-bit syndrome mask
+            for (long long l = 0; l < 64 && ok; ++l) {
+                const long long e0 = row_ptr[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, row_ptr[rb[w + 1]]);
+                int starts = 0;
+                for (int j = rb[w]; j < rb[w + 1]; ++j)
+                    if (row_ptr[j] >= e0 && row_ptr[j] < e1) ++starts;
+                ok = starts <= 32;
+            }
         }
         if (!ok) continue;
         g.variant = VAR_V2;
@@ -244,8 +254,14 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     const int G4 = v2 ? g->v2R / 4 : (reg ? EPL_REG / 4 : (EPL + 3) / 4);
     const int TS = reg ? REG_TSTRIDE : T;
     std::vector<uint32_t> meta((size_t)G4 * TS * 4, 0);
-    std::vector<int32_t> lrow0(T, -1), lhead(T, 0);
+    std::vector<int32_t> lrow0(T, v2 ? 0 : -1), lhead(T, 0), lnst(T, 0), lepl(T, EPL);
     // Lane l holds edges [e_begin, e_end) of its wave (v1: one "wave" of T lanes).
+    // V2 metadata differs in three ways: the END of a lane's tail (a row begun
+    // in the lane before) is cleared — the kernel finishes split rows after a
+    // shuffle; slots past the lane's edges up to the group count are dummy
+    // edges (column n, kpos 63, no flags), so every lane of a wave runs the
+    // same slots; lanes count the rows they start (lane_nst).
+    const uint32_t DUMMY = (uint32_t)n | (63u << META_KPOS_SHIFT);
     const int W = v2 ? T / 64 : 1;
     for (int w = 0; w < W; ++w) {
         const long long wb = v2 ? row_ptr[g->wave_rows[w]] : 0;
@@ -255,22 +271,32 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         for (int li = 0; li < lanes; ++li) {
             const int l = w * 64 + li;
             const long long e0 = wb + (long long)li * epl_w;
+            if (v2) lepl[l] = epl_w;
+            int head = 0;
             if (e0 < we) {
                 const int r0 = row_of[e0];
                 lrow0[l] = r0;
-                if (e0 != row_ptr[r0]) lhead[l] = row_ptr[r0 + 1] - (int)e0;
+                if (e0 != row_ptr[r0]) head = lhead[l] = row_ptr[r0 + 1] - (int)e0;
             }
             int prev_row = -1;
-            for (int k = 0; k < epl_w; ++k) {
+            for (int k = 0; k < (v2 ? G4 * 4 : epl_w); ++k) {
                 const long long e = e0 + k;
-                if (e >= we) break;
-                const int j = row_of[e];
-                uint32_t wd = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
-                if (e == row_ptr[j]) wd |= META_START;
-                if (e == row_ptr[j + 1] - 1) wd |= META_END;
-                if (k > 0 && j != prev_row && j != prev_row + 1)
-                    return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
-                prev_row = j;
+                uint32_t wd;
+                if (k >= epl_w || e >= we) {
+                    if (!v2) break;
+                    wd = DUMMY;
+                } else {
+                    const int j = row_of[e];
+                    wd = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
+                    if (e == row_ptr[j]) {
+                        wd |= META_START;
+                        ++lnst[l];
+                    }
+                    if (e == row_ptr[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
+                    if (k > 0 && j != prev_row && j != prev_row + 1)
+                        return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
+                    prev_row = j;
+                }
                 meta[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = wd;
             }
         }
@@ -306,7 +332,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         HIP_TRY(hipDeviceGetAttribute(&dg->num_cus, hipDeviceAttributeMultiprocessorCount, d));
         int rc;
         if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->lane_row0, lrow0)) ||
-            (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->ell_col, ell)) ||
+            (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
+            (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso))) {
             (void)hipSetDevice(prev);
             return rc;
@@ -397,6 +424,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     DecodeArgs a{};
     a.n = g->n; a.m = g->m; a.E = g->E; a.T = g->T; a.EPL = g->EPL; a.dv_max = g->dv_max; a.max_dc = g->max_dc;
     a.slot_meta = dg->slot_meta; a.lane_row0 = dg->lane_row0; a.lane_head = dg->lane_head;
+    a.lane_nst = dg->lane_nst; a.lane_epl = dg->lane_epl;
     a.ell_col = dg->ell_col; a.row_deg = dg->row_deg;
     a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
     a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
@@ -531,6 +559,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->slot_meta);
         (void)hipFree(d->lane_row0);
         (void)hipFree(d->lane_head);
+        (void)hipFree(d->lane_nst);
+        (void)hipFree(d->lane_epl);
         (void)hipFree(d->ell_col);
         (void)hipFree(d->row_deg);
         (void)hipFree(d->iso_bits);

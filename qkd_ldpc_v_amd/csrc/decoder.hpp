@@ -49,6 +49,8 @@ struct DecodeArgs {
     const uint32_t *slot_meta;  // [ceil(EPL/4)][T][4]: uint4 per 4 slots
     const int32_t *lane_row0;   // [T] row of slot 0 (or -1)
     const int32_t *lane_head;   // [T] leading slots that finish a row begun in lane-1
+    const int32_t *lane_nst;    // [T] V2: rows started in the lane
+    const int32_t *lane_epl;    // [T] V2: slots of the lane's wave (uniform per wave)
     const int32_t *ell_col;     // [max_dc][m] bit ids of each row, row-ELL, slot-major
     const int32_t *row_deg;     // [m]
     // decoder parameters
@@ -92,7 +94,7 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
                                hipStream_t stream);
 
-size_t lds_bytes_v2(int alg, int n, int m);
+size_t lds_bytes_v2(int alg, int n, int m, int T);
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,

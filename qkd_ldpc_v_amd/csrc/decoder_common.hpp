@@ -128,6 +128,27 @@ struct MetaSrc {
         }
     }
 };
+// Same, but only the slots a wave actually holds: `epl_s` is wave-uniform (an
+// SGPR), so each slot costs a scalar compare-and-branch, no VALU.  Slots past
+// a lane's last row are dummies, but a lane whose last row continues into the
+// next lane must never see one (it would enter that row's running product).
+template <int R>
+struct MetaSrcW : MetaSrc<R> {
+    template <typename F>
+    __device__ __forceinline__ void each_upto(int epl_s, F &&f) const {
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            if (4 * g < epl_s) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
+                f(4 * g + 0, (uint32_t)q[0]);
+                if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1]);
+                if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2]);
+                if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3]);
+            }
+        }
+    }
+};
+
 template <>
 struct MetaSrc<0> {
     const uint4 *mp;

@@ -28,24 +28,30 @@ constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
 
 __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// LDS of one frame.  total has n + 1 entries: total[n] is the column of the
+// dummy slots that pad every lane of a wave to the same slot count.
 struct V2Layout {
-    size_t total, rowA, rowB, rowflag, codes, palette, bytes;
-    __host__ __device__ V2Layout(int n, int m, int nc, bool minsum) {
+    size_t total, rows, rowflag, tail, tailneg, codes, palette, bytes;
+    __host__ __device__ V2Layout(int n, int m, int nc, int T, bool minsum) {
         size_t o = V2_CTRL;
-        total = o; o = al16(o + (size_t)n * 8);
-        rowA = o; o = al16(o + (size_t)m * 8);
-        rowB = o; o = al16(o + (minsum ? (size_t)m * 8 : 0));
+        total = o; o = al16(o + (size_t)(n + 1) * 8);
+        rows = o; o = al16(o + (size_t)m * (minsum ? 16 : 8));  // SPA: product; min-sum: {min1, min2}
         palette = o; o = al16(o + 4 * 8);
-        rowflag = o; o = al16(o + (size_t)m);
+        rowflag = o; o = al16(o + (minsum ? (size_t)m : 0));
+        tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
+        tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
         codes = o; o = al16(o + (size_t)nc);
         bytes = o;
     }
 };
 
-// Threads per workgroup each instantiation is built for: 16 waves at 44 slots
-// (128 VGPRs), 12 waves at 56 (168).
 template <int R>
 constexpr int v2_max_threads() { return v2_threads_for(R); }
+
+// Slots that can belong to a lane's tail (the end of a row begun in the lane
+// before): the planner keeps max_dc <= 32, so head <= 31.
+template <int R>
+constexpr int v2_tail_slots() { return R < 32 ? R : 32; }
 
 template <int ALG, int R>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
@@ -53,26 +59,35 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
     constexpr bool ADAPT = (ALG == 4 || ALG == 5);
     constexpr bool NORM = (ALG == 2 || ALG == 4);
+    constexpr int KT = v2_tail_slots<R>();
 
     const int tid = threadIdx.x;
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
-    const double thr = a.thr;
-    const bool thr_on = a.thr_on != 0;
-    const V2Layout L(n, m, nc, !SPA_FAM);
+    // threshold_matrix disabled == clipping at +inf (|v| > inf never holds; NaN passes)
+    const double thr = a.thr_on ? a.thr : __builtin_inf();
+    const V2Layout L(n, m, nc, T, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
     double *total = reinterpret_cast<double *>(smem + L.total);
-    double *rowA = reinterpret_cast<double *>(smem + L.rowA);
-    double *rowB = reinterpret_cast<double *>(smem + L.rowB);
+    double *rowA = reinterpret_cast<double *>(smem + L.rows);   // SPA
+    double2 *rowAB = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
     double *pal = reinterpret_cast<double *>(smem + L.palette);
-    uint8_t *rowflag = smem + L.rowflag;  // bit0 target syndrome, bit1 row mismatch, bit2 neg parity
+    uint8_t *rowflag = smem + L.rowflag;  // min-sum: bit0 syndrome, bit1 row mismatch, bit2 negative parity
+    double2 *tailagg = reinterpret_cast<double2 *>(smem + L.tail);
+    int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
     uint8_t *codes = smem + L.codes;
 
     EdgeMsgs<R> c2b;
-    MetaSrc<R> meta;
+    MetaSrcW<R> meta;
     meta.init(a.slot_meta, tid, T);
+    // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
+    // rows started here, and the wave's slot count (uniform across the wave).
     const int head_in = a.lane_head[tid];
     const int row0_in = a.lane_row0[tid];
+    const int nst = a.lane_nst[tid];
+    const int epl = __builtin_amdgcn_readfirstlane(a.lane_epl[tid]);
+    const int lane = tid & 63;
+    const int up = (lane == 0) ? 0 : lane - 1;
     int epoch = 0;
     if (tid == 0) *s_flag = 0;
 
@@ -82,7 +97,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const int f = *s_frame;
         if (f >= a.batch) break;
         const uint8_t *sy = a.synd + (size_t)f * m;
-        for (int j = tid; j < m; j += T) rowflag[j] = sy[j] & 1;
+        // Target syndrome bits of the rows this lane starts (bit i = i-th START),
+        // and of the row it finishes for the lane before (split row).
+        uint32_t smask_f = 0;
+        {
+            const int rs = row0_in + (head_in > 0 ? 1 : 0);
+            for (int i = 0; i < nst; ++i) smask_f |= (uint32_t)(sy[rs + i] & 1) << i;
+        }
+        const int s_row0 = (head_in > 0) ? (sy[row0_in] & 1) : 0;
         const bool paletted = a.pal_ok[f] != 0;
         // Non-paletted frames gather llr[] through a buffer resource: a distinct
         // load kind the compiler cannot fuse with the LDS palette read into a
@@ -102,6 +124,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // total starts as the channel LLRs: the check-node scan of iteration 0
         // reads the channel decision from it, and bits of degree 0 keep it.
         for (int i = tid; i < n; i += T) total[i] = llr_of(i);
+        if (tid == 0) total[n] = 1.0;  // dummy column
         __syncthreads();
 
         int iters = a.max_it, okv = 0;
@@ -111,100 +134,102 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             const bool compute = it < a.max_it;
             ++epoch;
             int head = head_in, row0 = row0_in;
-            asm volatile("" : "+v"(head), "+v"(row0));
+            uint32_t sm = smask_f;
+            asm volatile("" : "+v"(head), "+v"(row0), "+v"(sm));
 
             // ---- check-node scan: b2c, tanh / aggregates, row parity of z ----
+            // A START begins a row (bit `sm & 1` of the target syndrome); an END
+            // (set only on rows begun in this lane) publishes it.  Slots before
+            // the first START are the tail of the previous lane's last row.
             int r = row0;
-            double acc = 0.0;
-            MinAgg ag, hag;
-            agg_init(ag);
-            agg_init(hag);
-            int par = 0, hpar = 0;
-            bool tail_open = false;
-            meta.each(0, [&](int k, uint32_t mt) {
-                if (!(mt & META_VALID)) return;
-                const bool start = (mt & META_START) != 0;
-                if (k > 0 && start) ++r;
+            int par = 0, cur_s = 0, mis = 0, neg = 0;
+            uint32_t zt = 0;  // decisions of the first KT slots (tail parity)
+            double acc = 1.0, m1 = DBL_MAX, m2 = DBL_MAX;
+            meta.each_upto(epl, [&](int k, uint32_t mt) {
                 const int col = (int)(mt & META_COL_MASK);
                 const double tv = total[col];
                 const int zb = (tv <= 0.0) ? 1 : 0;
+                if (k < KT) zt |= (uint32_t)zb << k;
                 double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
                 if (had_vn) {
-                    x = tv - c2b.get(k);  // (:115)
-                    if (thr_on) x = clip_msg(x, thr);
+                    x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
                 }
-                double t = x;
+                const bool start = (mt & META_START) != 0;
+                const int s = (int)(sm & 1u);
                 if constexpr (SPA_FAM) {
+                    double t = x;
                     if (compute) t = (ALG == 0) ? ql_exact::tanh_dec(x / 2.) : tanh_lin(x / 2.);
-                }
-                c2b.set(k, t);
-                if (k < head) {  // tail of a row begun in the previous lane
-                    hpar ^= zb;
-                    if constexpr (!SPA_FAM) agg_push(hag, x);
-                    return;
-                }
-                if (start) {
-                    par = 0;
-                    if constexpr (!SPA_FAM) agg_init(ag);
-                }
-                par ^= zb;
-                if constexpr (SPA_FAM) {
-                    if (start) acc = ((rowflag[r] & 1) ? -1. : 1.) * t;  // (:57-62)
-                    else acc = acc * t;
+                    c2b.set(k, t);
+                    const double st = (s ? -1. : 1.) * t;  // (:57-62)
+                    acc = start ? st : acc * t;
                 } else {
-                    agg_push(ag, x);
+                    c2b.set(k, x);
+                    if (!SPA_FAM && k < KT && k > 0) {
+                        // the first START closes the tail segment: keep its aggregate
+                        if (k == head) {
+                            tailagg[tid] = make_double2(m1, m2);
+                            tailneg[tid] = neg;
+                        }
+                    }
+                    m1 = start ? DBL_MAX : m1;
+                    m2 = start ? DBL_MAX : m2;
+                    neg = start ? 0 : neg;
+                    // agg_push (:381-397), branch-free
+                    neg ^= (x < 0) ? 1 : 0;
+                    const double ax = __builtin_fabs(x);
+                    const bool lt1 = ax < m1, lt2 = ax < m2;
+                    m2 = lt1 ? m1 : (lt2 ? ax : m2);
+                    m1 = lt1 ? ax : m1;
                 }
+                cur_s = start ? s : cur_s;
+                sm = start ? (sm >> 1) : sm;
+                par = (start ? 0 : par) ^ zb;
+                if (k > 0) r += start ? 1 : 0;
                 if (mt & META_END) {
-                    const int fl = rowflag[r];
-                    const int mis = (par ^ fl) & 1;
+                    const int mr = par ^ cur_s;
+                    mis |= mr;
                     if constexpr (SPA_FAM) {
                         rowA[r] = acc;
-                        rowflag[r] = (uint8_t)((fl & 1) | (mis << 1));
                     } else {
-                        rowA[r] = ag.m1;
-                        rowB[r] = ag.m2;
-                        rowflag[r] = (uint8_t)((fl & 1) | (mis << 1) | (ag.neg << 2));
+                        rowAB[r] = make_double2(m1, m2);
+                        rowflag[r] = (uint8_t)(cur_s | (mr << 1) | (neg << 2));
                     }
-                    if (mis) *s_flag = epoch;
                 }
-                tail_open = !(mt & META_END);
             });
             // ---- rows split across two lanes of this wave: one shuffle ----
             {
-                const int lane = tid & 63;
-                const int up = (lane == 0) ? 0 : lane - 1;
-                const int ppar = __shfl(tail_open ? par : 0, up, 64);
+                const int ppar = __shfl(par, up, 64);
+                const int hpar = __builtin_popcount(zt & ((1u << head) - 1u)) & 1;
                 if constexpr (SPA_FAM) {
                     const double pacc = __shfl(acc, up, 64);
                     if (head > 0) {
-                        double p = pacc;
-                        if constexpr (R > 0) {
+                        double p = pacc;  // continue the row's product in CSR order
 #pragma unroll
-                            for (int k = 0; k < R; ++k)
-                                if (k < head) p = p * c2b.get(k);
-                        }
-                        const int fl = rowflag[row0];
-                        const int mis = (ppar ^ hpar ^ fl) & 1;
+                        for (int k = 0; k < KT; ++k)
+                            if (k < head) p = p * c2b.get(k);
                         rowA[row0] = p;
-                        rowflag[row0] = (uint8_t)((fl & 1) | (mis << 1));
-                        if (mis) *s_flag = epoch;
+                        mis |= ppar ^ hpar ^ s_row0;
                     }
                 } else {
                     MinAgg t;
-                    t.m1 = __shfl(ag.m1, up, 64);
-                    t.m2 = __shfl(ag.m2, up, 64);
-                    t.neg = __shfl(ag.neg, up, 64);
+                    t.m1 = __shfl(m1, up, 64);
+                    t.m2 = __shfl(m2, up, 64);
+                    t.neg = __shfl(neg, up, 64);
                     if (head > 0) {
-                        agg_merge(t, hag);
-                        const int fl = rowflag[row0];
-                        const int mis = (ppar ^ hpar ^ fl) & 1;
-                        rowA[row0] = t.m1;
-                        rowB[row0] = t.m2;
-                        rowflag[row0] = (uint8_t)((fl & 1) | (mis << 1) | (t.neg << 2));
-                        if (mis) *s_flag = epoch;
+                        const double2 ta = tailagg[tid];
+                        MinAgg h;
+                        h.m1 = ta.x;
+                        h.m2 = ta.y;
+                        h.neg = tailneg[tid];
+                        agg_merge(t, h);
+                        const int mr = ppar ^ hpar ^ s_row0;
+                        rowAB[row0] = make_double2(t.m1, t.m2);
+                        rowflag[row0] = (uint8_t)(s_row0 | (mr << 1) | (t.neg << 2));
+                        mis |= mr;
                     }
                 }
             }
+            if (mis) *s_flag = epoch;
             __syncthreads();
             const bool anymis = *s_flag == epoch;
             if (check && !anymis) {
@@ -216,23 +241,22 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
             // ---- check-to-bit messages + VN phase 0 (total = llr + first message) ----
             r = row0;
-            meta.each(0, [&](int k, uint32_t mt) {
-                if (!(mt & META_VALID)) return;
-                if (k > 0 && (mt & META_START)) ++r;
+            meta.each_upto(epl, [&](int k, uint32_t mt) {
+                if (k > 0) r += (mt & META_START) ? 1 : 0;
                 double c;
                 if constexpr (SPA_FAM) {
                     const double prod = rowA[r] / c2b.get(k);  // :66
                     c = 2. * ((ALG == 0) ? ql_exact::atanh_dec(prod) : atanh_lin(prod));
                 } else {
                     const double x = c2b.get(k);
+                    const double2 ab = rowAB[r];
                     const int fl = rowflag[r];
-                    double sp = (fl & 1) ? -1. : 1.;                   // :376
-                    sp *= ((fl >> 2) & 1) ? -1. : 1.;                  // :398
-                    const double prod = sp * ((x > 0) ? 1. : -1.);     // :402
-                    const double m1 = rowA[r];
-                    const double sel = (fabs(x) == m1) ? rowB[r] : m1; // :406
+                    // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
+                    const int sb = (fl ^ (fl >> 2) ^ ((x > 0) ? 0 : 1)) & 1;
+                    const double prod = sb ? -1. : 1.;
+                    const double sel = (__builtin_fabs(x) == ab.x) ? ab.y : ab.x;  // :406
                     double fac = a.primary;
-                    if (ADAPT && (fl & 2)) fac = a.secondary;          // :749-757
+                    if (ADAPT && (fl & 2)) fac = a.secondary;  // :749-757
                     if constexpr (NORM) {
                         c = fac * prod * sel;
                     } else {
@@ -240,7 +264,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         c = prod * ((d < 0.) ? 0. : d);
                     }
                 }
-                if (thr_on) c = clip_msg(c, thr);
+                c = clip_msg(c, thr);  // (:73-74)
                 c2b.set(k, c);
                 if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == 0) {
                     const int col = (int)(mt & META_COL_MASK);
@@ -250,8 +274,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             __syncthreads();
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
             for (int kk = 1; kk < a.dv_max; ++kk) {
-                meta.each(0, [&](int k, uint32_t mt) {
-                    if ((mt & META_VALID) && ((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
+                meta.each_upto(epl, [&](int k, uint32_t mt) {
+                    if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
                         const int col = (int)(mt & META_COL_MASK);
                         total[col] = total[col] + c2b.get(k);
                     }
@@ -356,8 +380,8 @@ KernelFn kernel_v2(int R, int alg) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m) {
-    return V2Layout(n, m, (n + 3) / 4, alg >= 2).bytes;
+size_t lds_bytes_v2(int alg, int n, int m, int T) {
+    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2).bytes;
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {

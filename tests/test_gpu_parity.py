@@ -282,3 +282,45 @@ def test_repeat_calls_deterministic(gpu_available):
     r1 = g.decode(p, llr, s, posterior=True)
     r2 = g.decode(p, llr, s, posterior=True)
     assert np.array_equal(r1.bits, r2.bits) and bits_equal_nan(r1.posterior, r2.posterior)
+
+
+def test_cpp_mirror_six_decoders_and_batch(gpu_available, tmp_path):
+    """The C++ mirror (reference names/signatures) end to end: each per-frame
+    decoder and decode_batch agree, and both equal the oracle."""
+    import subprocess
+
+    from conftest import ROOT
+
+    name = "c1_n1024_m220.alist"
+    H = load_fixture(name)
+    _, _, llr, s = frames(H, 0.03, 6, 123)
+    fr = tmp_path / "frames.bin"
+    with open(fr, "wb") as f:
+        f.write(np.int32(llr.shape[0]).tobytes())
+        for i in range(llr.shape[0]):
+            f.write(llr[i].astype(np.float64).tobytes())
+            f.write(s[i].astype(np.int32).tobytes())
+    out = tmp_path / "out.bin"
+    exe = f"{ROOT}/qkd_ldpc_v_amd/host/host_mirror_check"
+    r = subprocess.run([exe, "decoders", matrix_path(name), "1", str(fr), str(out)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+    raw = np.fromfile(out, np.uint8)
+    rec = 5 + H.n
+    O = Oracle(H)
+    for k, (alg, prim, sec) in enumerate(ALGS):
+        ob, oi, ok, _ = O.decode_batch(O.params(alg, 50, True, 100.0, prim, sec), llr, s, threads=4)
+        for f in range(llr.shape[0]):
+            b = raw[(k * llr.shape[0] + f) * rec:(k * llr.shape[0] + f + 1) * rec]
+            assert int(b[:4].view(np.uint32)[0]) == oi[f] and b[4] == ok[f]
+            assert np.array_equal(b[5:], ob[f])
+
+
+def test_cpp_mirror_kat(gpu_available):
+    import subprocess
+
+    from conftest import ROOT
+
+    exe = f"{ROOT}/qkd_ldpc_v_amd/host/host_mirror_check"
+    r = subprocess.run([exe, "kat", matrix_path("kat_n6_m4.dense")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "iterations=1 syndromes_match=1 keys_match=1", r.stdout
