@@ -37,6 +37,9 @@ WORKLOADS = {
     "c1": ("c1_n1024_m220.alist", 1, 0, 0.0, 0.0, 0.013, 4096, "C1: n=1k R~0.8 SPA 50-iter"),
     "c4": ("c4s_n102400_m32001.alist", 1, 0, 0.0, 0.0, 0.038, 128,
            "C4 stand-in: n=100k R=0.69 SPA 50-iter, batch 128/GPU (R=0.79 file absent upstream)"),
+    "c5": ("c5_n10240_m2048.sp2", 3, 5, 0.7, 0.99, 0.0156, 4096,
+           "C5 decode: n=10k R=0.8 irregular (matrices_2, format 3) AOMSA beta=0.7 sigma=0.99 "
+           "(configs/ADAPTIVE T.json, rate bucket 0.805) 50-iter, QBER 1.56%, batch 4096/GPU, no rate adaptation"),
 }
 
 

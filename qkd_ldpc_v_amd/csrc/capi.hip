@@ -72,6 +72,8 @@ struct DeviceGraph {
     uint32_t *slot_meta = nullptr;
     int32_t *lane_row0 = nullptr, *lane_head = nullptr, *ell_col = nullptr, *row_deg = nullptr;
     int32_t *lane_nst = nullptr, *lane_epl = nullptr;
+    uint32_t *slot_meta_ms = nullptr;                  // V2 min-sum: rows listed by kpos
+    uint64_t *vn_mask = nullptr, *vn_mask_ms = nullptr; // V2: [wave][dv_max] slot masks
     int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
@@ -83,7 +85,7 @@ struct DeviceGraph {
 
 struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
-    int v2R = 0, n_iso = 0;                 // V2: register slots per lane, bits of degree 0
+    int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
     std::vector<int> wave_rows;             // V2: first row of each wave (+ m)
     std::vector<std::unique_ptr<DeviceGraph>> devs;
 };
@@ -147,8 +149,10 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         if (row_ptr[j + 1] == row_ptr[j]) return false;  // empty rows: v1 checks them by row-ELL
     const long long E = g.E;
     const int forced = env_int("QLDPC_V2_WAVES", 0);
-    for (int R : {V2_R_SMALL, V2_R_MID}) {
-        const int wmax = v2_threads_for(R) / 64;
+    const int shapes[3][2] = {{V2_R_SMALL, 0}, {V2_R_MID, 0}, {V2_R_SMALL, V2_RG_HYBRID}};
+    for (const auto &sh : shapes) {
+        const int R = sh[0] + sh[1];  // slots per lane
+        const int wmax = v2_threads_for(sh[0]) / 64;
         int W = forced > 0 ? forced : (int)std::min<long long>(wmax, (E + 64LL * g.max_dc - 1) / (64LL * g.max_dc));
         W = std::max(1, W);
         if (W > wmax) continue;
@@ -181,7 +185,8 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         }
         if (!ok) continue;
         g.variant = VAR_V2;
-        g.v2R = R;
+        g.v2R = sh[0];
+        g.v2RG = sh[1];
         g.T = W * 64;
         g.EPL = epl;
         g.wave_rows = rb;
@@ -251,7 +256,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // have a fixed group count at lane stride REG_TSTRIDE.
     const bool v2 = g->variant == VAR_V2;
     const bool reg = g->variant == VAR_REG_LDS || v2;
-    const int G4 = v2 ? g->v2R / 4 : (reg ? EPL_REG / 4 : (EPL + 3) / 4);
+    const int G4 = v2 ? (g->v2R + g->v2RG) / 4 : (reg ? EPL_REG / 4 : (EPL + 3) / 4);
     const int TS = reg ? REG_TSTRIDE : T;
     std::vector<uint32_t> meta((size_t)G4 * TS * 4, 0);
     std::vector<int32_t> lrow0(T, v2 ? 0 : -1), lhead(T, 0), lnst(T, 0), lepl(T, EPL);
@@ -263,44 +268,67 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // same slots; lanes count the rows they start (lane_nst).
     const uint32_t DUMMY = (uint32_t)n | (63u << META_KPOS_SHIFT);
     const int W = v2 ? T / 64 : 1;
-    for (int w = 0; w < W; ++w) {
-        const long long wb = v2 ? row_ptr[g->wave_rows[w]] : 0;
-        const long long we = v2 ? row_ptr[g->wave_rows[w + 1]] : E;
-        const int lanes = v2 ? 64 : T;
-        const int epl_w = v2 ? std::max<int>((int)((we - wb + 63) / 64), g->max_dc) : EPL;
-        for (int li = 0; li < lanes; ++li) {
-            const int l = w * 64 + li;
-            const long long e0 = wb + (long long)li * epl_w;
-            if (v2) lepl[l] = epl_w;
-            int head = 0;
-            if (e0 < we) {
-                const int r0 = row_of[e0];
-                lrow0[l] = r0;
-                if (e0 != row_ptr[r0]) head = lhead[l] = row_ptr[r0 + 1] - (int)e0;
-            }
-            int prev_row = -1;
-            for (int k = 0; k < (v2 ? G4 * 4 : epl_w); ++k) {
-                const long long e = e0 + k;
-                uint32_t wd;
-                if (k >= epl_w || e >= we) {
-                    if (!v2) break;
-                    wd = DUMMY;
-                } else {
-                    const int j = row_of[e];
-                    wd = (uint32_t)col_idx[e] | ((uint32_t)kpos[e] << META_KPOS_SHIFT) | META_VALID;
-                    if (e == row_ptr[j]) {
-                        wd |= META_START;
-                        ++lnst[l];
-                    }
-                    if (e == row_ptr[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
-                    if (k > 0 && j != prev_row && j != prev_row + 1)
-                        return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
-                    prev_row = j;
+    // V2 min-sum metadata lists each row's edges by kpos: the min-sum row
+    // aggregate and parity are order-free, and grouping a
+    // row's k-th bit edges lets the VN phase masks skip more slots.  SPA keeps
+    // CSR order (its row product is sequential, :57-62).
+    std::vector<int> perm(E);
+    for (int e = 0; e < E; ++e) perm[e] = e;
+    auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm) -> int {
+        mt.assign((size_t)G4 * TS * 4, 0);
+        vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
+        if (sorted)
+            for (int j = 0; j < m; ++j)
+                std::stable_sort(perm.begin() + row_ptr[j], perm.begin() + row_ptr[j + 1],
+                                 [&](int x, int y) { return kpos[x] < kpos[y]; });
+        for (int w = 0; w < W; ++w) {
+            const long long wb = v2 ? row_ptr[g->wave_rows[w]] : 0;
+            const long long we = v2 ? row_ptr[g->wave_rows[w + 1]] : E;
+            const int lanes = v2 ? 64 : T;
+            const int epl_w = v2 ? std::max<int>((int)((we - wb + 63) / 64), g->max_dc) : EPL;
+            for (int li = 0; li < lanes; ++li) {
+                const int l = w * 64 + li;
+                const long long e0 = wb + (long long)li * epl_w;
+                if (v2) lepl[l] = epl_w;
+                int head = 0;
+                lnst[l] = 0;
+                if (e0 < we) {
+                    const int r0 = row_of[e0];
+                    lrow0[l] = r0;
+                    if (e0 != row_ptr[r0]) head = lhead[l] = row_ptr[r0 + 1] - (int)e0;
                 }
-                meta[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = wd;
+                int prev_row = -1;
+                for (int k = 0; k < (v2 ? G4 * 4 : epl_w); ++k) {
+                    const long long e = e0 + k;  // position in the row-major edge list
+                    uint32_t wd;
+                    if (k >= epl_w || e >= we) {
+                        if (!v2) break;
+                        wd = DUMMY;
+                    } else {
+                        const int j = row_of[e];
+                        const int ed = perm[e];  // the edge at that position
+                        wd = (uint32_t)col_idx[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
+                        if (v2) vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
+                        if (e == row_ptr[j]) {
+                            wd |= META_START;
+                            ++lnst[l];
+                        }
+                        if (e == row_ptr[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
+                        if (k > 0 && j != prev_row && j != prev_row + 1)
+                            return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
+                        prev_row = j;
+                    }
+                    mt[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = wd;
+                }
             }
         }
-    }
+        return QLDPC_OK;
+    };
+    std::vector<uint32_t> meta_ms;
+    std::vector<uint64_t> vnm, vnm_ms;
+    int brc = build_meta(false, meta, vnm);
+    if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms);
+    if (brc) return brc;
     // Row-ELL (slot-major) for syndrome evaluation.
     const int dcm = std::max(1, g->max_dc);
     std::vector<int32_t> ell((size_t)dcm * std::max(m, 1), 0), rdeg(std::max(m, 1), 0);
@@ -331,7 +359,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         HIP_TRY(hipSetDevice(d));
         HIP_TRY(hipDeviceGetAttribute(&dg->num_cus, hipDeviceAttributeMultiprocessorCount, d));
         int rc;
-        if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->lane_row0, lrow0)) ||
+        if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->slot_meta_ms, meta_ms)) ||
+            (rc = upload(&dg->vn_mask, vnm)) || (rc = upload(&dg->vn_mask_ms, vnm_ms)) ||
+            (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso))) {
@@ -394,7 +424,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         std::lock_guard<std::mutex> lk(dg->mu);
         if (dg->occ[alg] == 0) {
             int b = 0;
-            if (v2) HIP_TRY(occupancy_v2(g->v2R, alg, g->T, lds, &b));
+            if (v2) HIP_TRY(occupancy_v2(g->v2R, g->v2RG, alg, g->T, lds, &b));
             else HIP_TRY(occupancy(g->variant, alg, g->T, lds, &b));
             if (b <= 0) return fail(QLDPC_EUNSUP, "decoder kernel cannot be resident with this graph shape");
             dg->occ[alg] = b;
@@ -407,8 +437,10 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
                 return fail(QLDPC_EINVAL, "frame codes were not built for this batch");
             int rc = ensure_codes(g, w, batch, stream);
             if (rc) return rc;
-        } else {
-            const long long per = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+        }
+        {
+            const long long per = v2 ? (long long)g->v2RG * REG_TSTRIDE
+                                     : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
             const size_t need = (size_t)per * (size_t)wgs;
             if (need > w->scratch_doubles) {
                 if (w->scratch) {
@@ -425,16 +457,18 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.n = g->n; a.m = g->m; a.E = g->E; a.T = g->T; a.EPL = g->EPL; a.dv_max = g->dv_max; a.max_dc = g->max_dc;
     a.slot_meta = dg->slot_meta; a.lane_row0 = dg->lane_row0; a.lane_head = dg->lane_head;
     a.lane_nst = dg->lane_nst; a.lane_epl = dg->lane_epl;
+    if (v2 && alg >= 2) a.slot_meta = dg->slot_meta_ms;
+    a.vn_mask = (v2 && alg >= 2) ? dg->vn_mask_ms : dg->vn_mask;
     a.ell_col = dg->ell_col; a.row_deg = dg->row_deg;
     a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
     a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
     a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
     a.frame_counter = w->counter;
     a.scratch = w->scratch;
-    a.scratch_wg_doubles = v2 ? 0 : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.scratch_wg_doubles = v2 ? (long long)g->v2RG * REG_TSTRIDE : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
     a.nc = (g->n + 3) / 4;
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
-    a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R;
+    a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
     if (v2 && !codes_ready)
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
@@ -560,6 +594,9 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->lane_row0);
         (void)hipFree(d->lane_head);
         (void)hipFree(d->lane_nst);
+        (void)hipFree(d->slot_meta_ms);
+        (void)hipFree(d->vn_mask);
+        (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->lane_epl);
         (void)hipFree(d->ell_col);
         (void)hipFree(d->row_deg);
@@ -598,13 +635,13 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
     if (lanes) *lanes = g->T;
     if (edges_per_lane) *edges_per_lane = g->EPL;
     if (lds_bytes) *lds_bytes = (int32_t)lds;
-    if (variant) *variant = variant_name(g->variant);
+    if (variant) *variant = (g->variant == VAR_V2 && g->v2RG > 0) ? "v2_hybrid" : variant_name(g->variant);
     if (workgroups) {
         int prev = 0;
         HIP_TRY(hipGetDevice(&prev));
         HIP_TRY(hipSetDevice(dg->device));
         int b = 0;
-        hipError_t e = g->variant == VAR_V2 ? occupancy_v2(g->v2R, algorithm, g->T, lds, &b)
+        hipError_t e = g->variant == VAR_V2 ? occupancy_v2(g->v2R, g->v2RG, algorithm, g->T, lds, &b)
                                             : occupancy(g->variant, algorithm, g->T, lds, &b);
         (void)hipSetDevice(prev);
         if (e != hipSuccess) return hip_fail(e, "occupancy");

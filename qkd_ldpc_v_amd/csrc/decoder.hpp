@@ -31,6 +31,8 @@ enum Variant : int {
 // waves, holds no more edges than 56 x 12 and its SPA build falls back to a
 // scratch array, so it is not built.)
 constexpr int V2_R_SMALL = 44, V2_R_MID = 56;
+// Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
+constexpr int V2_RG_HYBRID = 20;
 // Workgroup size each V2 instantiation is compiled for (its VGPR budget).
 constexpr __host__ __device__ int v2_threads_for(int R) { return R <= V2_R_SMALL ? 1024 : 768; }
 
@@ -77,6 +79,8 @@ struct DecodeArgs {
     int n_iso;               // bits with no check (dv = 0): total = llr
     const int32_t *iso_bits; // [n_iso]
     int v2R;                 // register slots of the V2 instantiation to launch
+    int v2RG;                // + slots in per-workgroup global scratch (0 or V2_RG_HYBRID)
+    const uint64_t *vn_mask; // [waves][dv_max]: slots holding a kk-th bit edge, per wave
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -96,7 +100,7 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
 
 size_t lds_bytes_v2(int alg, int n, int m, int T);
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
-hipError_t occupancy_v2(int R, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
+hipError_t occupancy_v2(int R, int RG, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
                             uint8_t *pal_ok, hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);

@@ -92,6 +92,36 @@ struct EdgeMsgs<0> {  // per-workgroup global scratch, slot-major [k][lane]: coa
     __device__ __forceinline__ void set(int k, double x) { p[(size_t)k * T] = x; }
 };
 
+// V2 message storage: slots k < R in VGPRs, slots R <= k < R + RG in this
+// workgroup's global scratch, slot-major [k - R][lane] (lane stride
+// REG_TSTRIDE) — coalesced, constant offsets, L2/MALL-resident.  A lane only
+// ever reads back what it wrote itself, so program order suffices.
+template <int R, int RG>
+struct EdgeMsgsH {
+    double v[R];
+    __amdgpu_buffer_rsrc_t rs;
+    int voff;
+    __device__ __forceinline__ void bind(double *wg_base, int tid) {
+        if constexpr (RG > 0) {
+            rs = __builtin_amdgcn_make_buffer_rsrc((void *)wg_base, (short)0, RG * REG_TSTRIDE * 8, 0x00020000);
+            voff = tid * 8;
+        }
+    }
+    __device__ __forceinline__ double get(int k) const {
+        if (k < R) return v[k];
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (k - R) * REG_TSTRIDE * 8, 0));
+    }
+    __device__ __forceinline__ void set(int k, double x) {
+        if (k < R) {
+            v[k] = x;
+        } else {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), rs, voff, (k - R) * REG_TSTRIDE * 8,
+                                                  0);
+        }
+    }
+};
+
 // Visit this lane's slots in order, handing each slot's metadata word to f.
 // Metadata is one uint4 per four consecutive slots, group-major [g][lane], so a
 // wave reads 1 KiB contiguous per group.  The register variant uses a fixed
@@ -144,6 +174,21 @@ struct MetaSrcW : MetaSrc<R> {
                 if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1]);
                 if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2]);
                 if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3]);
+            }
+        }
+    }
+    template <typename F>
+    __device__ __forceinline__ void each_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            const uint32_t w = (4 * g < 32) ? mlo : mhi;
+            const int b = (4 * g) & 31;
+            if ((w >> b) & 15u) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
+                if ((w >> b) & 1u) f(4 * g + 0, (uint32_t)q[0]);
+                if ((w >> (b + 1)) & 1u) f(4 * g + 1, (uint32_t)q[1]);
+                if ((w >> (b + 2)) & 1u) f(4 * g + 2, (uint32_t)q[2]);
+                if ((w >> (b + 3)) & 1u) f(4 * g + 3, (uint32_t)q[3]);
             }
         }
     }

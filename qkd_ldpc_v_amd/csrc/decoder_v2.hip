@@ -48,18 +48,21 @@ struct V2Layout {
 template <int R>
 constexpr int v2_max_threads() { return v2_threads_for(R); }
 
-// Slots that can belong to a lane's tail (the end of a row begun in the lane
-// before): the planner keeps max_dc <= 32, so head <= 31.
-template <int R>
-constexpr int v2_tail_slots() { return R < 32 ? R : 32; }
+// R message slots per lane in VGPRs plus RG in global scratch; S = R + RG
+// slots in all.  Slots that can belong to a lane's tail (the end of a row
+// begun in the lane before): the planner keeps max_dc <= 32, so head <= 31.
+template <int S>
+constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 
-template <int ALG, int R>
+template <int ALG, int R, int RG>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
     constexpr bool ADAPT = (ALG == 4 || ALG == 5);
     constexpr bool NORM = (ALG == 2 || ALG == 4);
-    constexpr int KT = v2_tail_slots<R>();
+    constexpr int S = R + RG;
+    static_assert(S <= 64, "VN phase masks are 64-bit");
+    constexpr int KT = v2_tail_slots<S>();
 
     const int tid = threadIdx.x;
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
@@ -77,9 +80,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
     uint8_t *codes = smem + L.codes;
 
-    EdgeMsgs<R> c2b;
-    MetaSrcW<R> meta;
+    EdgeMsgsH<R, RG> c2b;
+    c2b.bind(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles, tid);
+    MetaSrcW<S> meta;
     meta.init(a.slot_meta, tid, T);
+    // VN phase kk visits only the slots where some lane of this wave holds the
+    // kk-th edge of a bit (capi.hip: vn_mask[wave][kk]).
+    const uint64_t *vn_mask = a.vn_mask + (size_t)(tid >> 6) * a.dv_max;
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
     const int head_in = a.lane_head[tid];
@@ -274,7 +281,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             __syncthreads();
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
             for (int kk = 1; kk < a.dv_max; ++kk) {
-                meta.each_upto(epl, [&](int k, uint32_t mt) {
+                const uint64_t vm = vn_mask[kk];
+                const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
+                const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
+                meta.each_masked(mlo, mhi, [&](int k, uint32_t mt) {
                     if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
                         const int col = (int)(mt & META_COL_MASK);
                         total[col] = total[col] + c2b.get(k);
@@ -359,23 +369,22 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
 
 using KernelFn = void (*)(DecodeArgs);
 
-template <int R>
+template <int R, int RG>
 KernelFn pick_v2(int alg) {
     switch (alg) {
-    case 0: return decode_v2_kernel<0, R>;
-    case 1: return decode_v2_kernel<1, R>;
-    case 2: return decode_v2_kernel<2, R>;
-    case 3: return decode_v2_kernel<3, R>;
-    case 4: return decode_v2_kernel<4, R>;
-    default: return decode_v2_kernel<5, R>;
+    case 0: return decode_v2_kernel<0, R, RG>;
+    case 1: return decode_v2_kernel<1, R, RG>;
+    case 2: return decode_v2_kernel<2, R, RG>;
+    case 3: return decode_v2_kernel<3, R, RG>;
+    case 4: return decode_v2_kernel<4, R, RG>;
+    default: return decode_v2_kernel<5, R, RG>;
     }
 }
 
-KernelFn kernel_v2(int R, int alg) {
-    switch (R) {
-    case V2_R_SMALL: return pick_v2<V2_R_SMALL>(alg);
-    default: return pick_v2<V2_R_MID>(alg);
-    }
+KernelFn kernel_v2(int R, int RG, int alg) {
+    if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
+    if (R == V2_R_SMALL) return pick_v2<V2_R_SMALL, 0>(alg);
+    return pick_v2<V2_R_MID, 0>(alg);
 }
 
 }  // namespace
@@ -385,7 +394,7 @@ size_t lds_bytes_v2(int alg, int n, int m, int T) {
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
-    KernelFn k = kernel_v2(a.v2R, a.alg);
+    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.alg);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
@@ -393,8 +402,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     return hipGetLastError();
 }
 
-hipError_t occupancy_v2(int R, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
-    KernelFn k = kernel_v2(R, alg);
+hipError_t occupancy_v2(int R, int RG, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
+    KernelFn k = kernel_v2(R, RG, alg);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;

@@ -179,9 +179,15 @@ def test_c3_10k(gpu_available, alg, prim, sec):
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-def test_c5_irregular_global_message_variant(gpu_available, alg, prim, sec):
-    assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "glb_lds"
+def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
+    assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
     assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.025, batch=12, seed=50 + alg)
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_c5_irregular_v1_global_message_variant(gpu_available, alg, prim, sec):
+    assert graph("c5_n10240_m2048.sp2", "v1").plan(0, alg)["variant"] == "glb_lds"
+    assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.025, batch=6, seed=60 + alg, variant="v1")
 
 
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.AOMSA, 0.55, 1.2)])
