@@ -74,6 +74,8 @@ struct DeviceGraph {
     int32_t *lane_nst = nullptr, *lane_epl = nullptr;
     uint32_t *slot_meta_ms = nullptr;                  // V2 min-sum: rows listed by kpos
     uint64_t *vn_mask = nullptr, *vn_mask_ms = nullptr; // V2: [wave][dv_max] slot masks
+    uint32_t *slot_meta2 = nullptr, *slot_meta2_ms = nullptr;  // V2 hybrid: stage index per slot
+    int32_t *hd_bits = nullptr, *hd_dv = nullptr, *stage_off = nullptr;
     int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
@@ -87,6 +89,8 @@ struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
     int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
     std::vector<int> wave_rows;             // V2: first row of each wave (+ m)
+    int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
+    long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     std::vector<std::unique_ptr<DeviceGraph>> devs;
 };
 
@@ -274,8 +278,32 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // CSR order (its row product is sequential, :57-62).
     std::vector<int> perm(E);
     for (int e = 0; e < E; ++e) perm[e] = e;
-    auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm) -> int {
+    // Hybrid shape: VN terms kk >= vn_k0 go through a per-frame stage, laid out
+    // term-major over the bits of degree > kk, bits ordered by degree
+    // (descending) so each term's bits are a prefix: stage[off[kk] + rank[b]].
+    g->vn_k0 = g->dv_max;
+    std::vector<int32_t> hd_bits, hd_dv, stage_off(std::max(1, g->dv_max), 0), rank(n, -1);
+    if (v2 && g->v2RG > 0 && g->dv_max > 4) {
+        g->vn_k0 = 4;
+        for (int i = 0; i < n; ++i)
+            if (dv[i] > g->vn_k0) hd_bits.push_back(i);
+        std::stable_sort(hd_bits.begin(), hd_bits.end(), [&](int x, int y) { return dv[x] > dv[y]; });
+        for (size_t i = 0; i < hd_bits.size(); ++i) {
+            rank[hd_bits[i]] = (int)i;
+            hd_dv.push_back(dv[hd_bits[i]]);
+        }
+        long long off = 0;
+        for (int kk = g->vn_k0; kk < g->dv_max; ++kk) {
+            stage_off[kk] = (int32_t)off;
+            for (int d : hd_dv) off += (d > kk) ? 1 : 0;
+        }
+        g->stage_doubles = off;
+    }
+    g->n_hd = (int)hd_bits.size();
+    auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm,
+                          std::vector<uint32_t> &mt2) -> int {
         mt.assign((size_t)G4 * TS * 4, 0);
+        mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
         if (sorted)
             for (int j = 0; j < m; ++j)
@@ -309,6 +337,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         const int ed = perm[e];  // the edge at that position
                         wd = (uint32_t)col_idx[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
                         if (v2) vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
+                        if (g->n_hd && kpos[ed] >= g->vn_k0)
+                            mt2[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] =
+                                (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
                         if (e == row_ptr[j]) {
                             wd |= META_START;
                             ++lnst[l];
@@ -324,11 +355,25 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
         return QLDPC_OK;
     };
-    std::vector<uint32_t> meta_ms;
+    std::vector<uint32_t> meta_ms, meta2, meta2_ms;
     std::vector<uint64_t> vnm, vnm_ms;
-    int brc = build_meta(false, meta, vnm);
-    if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms);
+    int brc = build_meta(false, meta, vnm, meta2);
+    if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms, meta2_ms);
     if (brc) return brc;
+    if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
+        auto visited = [&](const std::vector<uint64_t> &v) {
+            long long s = 0;
+            for (int w = 0; w < W; ++w)
+                for (int kk = 1; kk < g->dv_max; ++kk) s += __builtin_popcountll(v[(size_t)w * g->dv_max + kk]);
+            return s;
+        };
+        long long full = 0;
+        for (int w = 0; w < W; ++w) full += (long long)(g->dv_max - 1) * lepl[w * 64];
+        fprintf(stderr, "{\"plan\": {\"waves\": %d, \"slots_reg\": %d, \"slots_scratch\": %d, \"epl_max\": %d, "
+                        "\"dv_max\": %d, \"vn_slot_visits_csr\": %lld, \"vn_slot_visits_kpos_sorted\": %lld, "
+                        "\"vn_slot_visits_unmasked\": %lld}}\n",
+                W, g->v2R, g->v2RG, g->EPL, g->dv_max, visited(vnm), visited(vnm_ms), full);
+    }
     // Row-ELL (slot-major) for syndrome evaluation.
     const int dcm = std::max(1, g->max_dc);
     std::vector<int32_t> ell((size_t)dcm * std::max(m, 1), 0), rdeg(std::max(m, 1), 0);
@@ -361,6 +406,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         int rc;
         if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->slot_meta_ms, meta_ms)) ||
             (rc = upload(&dg->vn_mask, vnm)) || (rc = upload(&dg->vn_mask_ms, vnm_ms)) ||
+            (rc = upload(&dg->slot_meta2, meta2)) || (rc = upload(&dg->slot_meta2_ms, meta2_ms)) ||
+            (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
+            (rc = upload(&dg->stage_off, stage_off)) ||
             (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
@@ -387,6 +435,11 @@ int check_params(const qldpc_params *p) {
     if (p->max_iterations < 1) return fail(QLDPC_EINVAL, "max_iterations must be >= 1");
     if (p->thr_enabled && !(p->thr > 0.)) return fail(QLDPC_EINVAL, "threshold must be > 0 when enabled");
     return QLDPC_OK;
+}
+
+// Per-workgroup scratch of the V2 kernels: overflow message slots, then the VN stage.
+long long v2_scratch_doubles(const qldpc_graph &g) {
+    return ((long long)g.v2RG * REG_TSTRIDE + g.stage_doubles + 31) / 32 * 32;
 }
 
 // Per-stream workspace of a device graph, created on first use.
@@ -439,7 +492,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
             if (rc) return rc;
         }
         {
-            const long long per = v2 ? (long long)g->v2RG * REG_TSTRIDE
+            const long long per = v2 ? v2_scratch_doubles(*g)
                                      : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
             const size_t need = (size_t)per * (size_t)wgs;
             if (need > w->scratch_doubles) {
@@ -465,7 +518,10 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
     a.frame_counter = w->counter;
     a.scratch = w->scratch;
-    a.scratch_wg_doubles = v2 ? (long long)g->v2RG * REG_TSTRIDE : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.scratch_wg_doubles = v2 ? v2_scratch_doubles(*g) : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.vn_k0 = g->vn_k0; a.n_hd = g->n_hd; a.hd_bits = dg->hd_bits; a.hd_dv = dg->hd_dv; a.stage_off = dg->stage_off;
+    a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
+    a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.nc = (g->n + 3) / 4;
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
     a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
@@ -595,6 +651,11 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->lane_head);
         (void)hipFree(d->lane_nst);
         (void)hipFree(d->slot_meta_ms);
+        (void)hipFree(d->slot_meta2);
+        (void)hipFree(d->slot_meta2_ms);
+        (void)hipFree(d->hd_bits);
+        (void)hipFree(d->hd_dv);
+        (void)hipFree(d->stage_off);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->lane_epl);

@@ -81,6 +81,15 @@ struct DecodeArgs {
     int v2R;                 // register slots of the V2 instantiation to launch
     int v2RG;                // + slots in per-workgroup global scratch (0 or V2_RG_HYBRID)
     const uint64_t *vn_mask; // [waves][dv_max]: slots holding a kk-th bit edge, per wave
+    // V2 hybrid: VN terms k >= vn_k0 are staged in scratch by the message pass
+    // and summed per bit in one gather pass (bits sorted by degree, descending).
+    int vn_k0;                      // first staged term (dv_max: none)
+    int n_hd;                       // bits with degree > vn_k0
+    const int32_t *hd_bits;         // [n_hd]
+    const int32_t *hd_dv;           // [n_hd]
+    const int32_t *stage_off;       // [dv_max]: offset of term kk's block in the stage
+    const uint32_t *slot_meta2;     // like slot_meta: stage index of the slot's edge
+    long long stage_wg_offset;      // doubles from a workgroup's scratch base to its stage
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.

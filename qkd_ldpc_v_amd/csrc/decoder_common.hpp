@@ -177,6 +177,22 @@ struct MetaSrcW : MetaSrc<R> {
             }
         }
     }
+    // Same as each_upto, also handing over the word of a second metadata array
+    // of identical layout (rs2).
+    template <typename F>
+    __device__ __forceinline__ void each_upto2(int epl_s, __amdgpu_buffer_rsrc_t rs2, F &&f) const {
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            if (4 * g < epl_s) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
+                const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rs2, this->voff, g * REG_TSTRIDE * 16, 0);
+                f(4 * g + 0, (uint32_t)q[0], (uint32_t)q2[0]);
+                if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1], (uint32_t)q2[1]);
+                if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2], (uint32_t)q2[2]);
+                if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3], (uint32_t)q2[3]);
+            }
+        }
+    }
     template <typename F>
     __device__ __forceinline__ void each_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
 #pragma unroll

@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     constexpr bool NORM = (ALG == 2 || ALG == 4);
     constexpr int S = R + RG;
     static_assert(S <= 64, "VN phase masks are 64-bit");
+    constexpr bool GATHER = RG > 0;  // sparse VN terms through the stage (hybrid shape)
     constexpr int KT = v2_tail_slots<S>();
 
     const int tid = threadIdx.x;
@@ -87,6 +88,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // VN phase kk visits only the slots where some lane of this wave holds the
     // kk-th edge of a bit (capi.hip: vn_mask[wave][kk]).
     const uint64_t *vn_mask = a.vn_mask + (size_t)(tid >> 6) * a.dv_max;
+    double *stage = a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.stage_wg_offset;
+    // (only used by the GATHER instantiations)
+    const __amdgpu_buffer_rsrc_t stage_rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, GATHER ? 0x7fffffff : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.slot_meta2, (short)0, GATHER ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
+    const int k0 = GATHER ? a.vn_k0 : a.dv_max;
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
     const int head_in = a.lane_head[tid];
@@ -248,7 +256,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
             // ---- check-to-bit messages + VN phase 0 (total = llr + first message) ----
             r = row0;
-            meta.each_upto(epl, [&](int k, uint32_t mt) {
+            auto message = [&](int k, uint32_t mt, uint32_t mt2) {
                 if (k > 0) r += (mt & META_START) ? 1 : 0;
                 double c;
                 if constexpr (SPA_FAM) {
@@ -273,14 +281,27 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
                 c = clip_msg(c, thr);  // (:73-74)
                 c2b.set(k, c);
-                if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == 0) {
+                const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
+                if (kp == 0) {
                     const int col = (int)(mt & META_COL_MASK);
                     total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
                 }
-            });
+                if constexpr (GATHER) {
+                    if (kp >= (uint32_t)k0 && kp != 63u) {
+                        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, c), stage_rs, (int)(mt2 * 8),
+                                                              0, 0);
+                    }
+                }
+            };
+            if constexpr (GATHER) {
+                meta.each_upto2(epl, meta2_rs, message);
+            } else {
+                meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
+            }
             __syncthreads();
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
-            for (int kk = 1; kk < a.dv_max; ++kk) {
+            for (int kk = 1; kk < k0; ++kk) {
                 const uint64_t vm = vn_mask[kk];
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
                 const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
@@ -291,6 +312,19 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     }
                 });
                 __syncthreads();
+            }
+            if constexpr (GATHER) {
+                // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
+                if (k0 < a.dv_max) {
+                    for (int i = tid; i < a.n_hd; i += T) {
+                        const int b = a.hd_bits[i];
+                        const int dvb = a.hd_dv[i];
+                        double sacc = total[b];
+                        for (int kk = k0; kk < dvb; ++kk) sacc = sacc + stage[a.stage_off[kk] + i];
+                        total[b] = sacc;
+                    }
+                    __syncthreads();
+                }
             }
             had_vn = true;
         }
