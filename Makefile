@@ -17,13 +17,16 @@ $(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decode
 $(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/loaders.o: $(CSRC)/loaders.cpp $(CSRC)/loaders.hpp
 	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(LIB): $(CSRC)/decoder.o $(CSRC)/decoder_v2.o $(CSRC)/capi.o $(CSRC)/loaders.o
+$(LIB): $(CSRC)/decoder.o $(CSRC)/decoder_v2.o $(CSRC)/trials.o $(CSRC)/capi.o $(CSRC)/loaders.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
 # Diagnostic build with per-phase s_memtime stamps (never the product).
@@ -33,11 +36,11 @@ $(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/dec
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
-$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
+$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2.o $(CSRC)/trials.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
 	mkdir -p $(PKG)/diag
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
-$(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h
+$(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h oracle/trials_oracle.cpp
 	$(MAKE) -C oracle
 
 $(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)

@@ -43,6 +43,10 @@ WORKLOADS = {
 }
 
 
+# SIMULATION_SEED of the config each workload comes from (configs_all/*.json).
+SIMULATION_SEEDS = {"c1": 9012025, "c2": 1022025, "c3": 10022025}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -86,11 +90,20 @@ def main():
     plan = g.plan(local, alg)
     params = Q.Params(alg, args.max_iterations, True, 100.0, prim, sec)
 
-    # ---- trials (not timed): synthetic BSC keys, resident in HBM ----
-    a, b, q_acc = Q.bsc_frames(n, qber, batch, seed=rank_seed(rank))
+    # ---- trials (not timed): run_trial's keys, generated on device and resident in HBM ----
+    # The reference's generator (src/simulation.cpp:540-551,713-719,743):
+    # per-trial seeds drawn from Xoshiro256++(SIMULATION_SEED); each rank takes
+    # its own contiguous slice of trials.
+    seeds = Q.trial_seeds(SIMULATION_SEEDS.get(args.workload, 1022025), batch * world)[rank * batch:(rank + 1) * batch]
+    d_seeds = torch.from_numpy(seeds.view(np.int64)).to(dev)
+    ta = torch.empty((batch, n), dtype=torch.uint8, device=dev)
+    tb = torch.empty((batch, n), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    tg0 = time.perf_counter()
+    q_acc = Q.trials_device(n, qber, d_seeds, ta, tb)
+    torch.cuda.synchronize()
+    trial_gen_s = time.perf_counter() - tg0
     lp = Q.log_p(q_acc)
-    ta = torch.from_numpy(a).to(dev)
-    tb = torch.from_numpy(b).to(dev)
     tlp = torch.full((batch,), lp, dtype=torch.float64, device=dev)
     nst = max(1, args.streams)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nst - 1)]
@@ -168,8 +181,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic BSC sifted keys (exactly floor(n*QBER) flips per frame, numpy PCG64), "
+            "data": "synthetic sifted keys from the reference's own trial generator (Xoshiro256++ seeds, "
+                    "exactly floor(n*QBER) errors, libstdc++ draw semantics) run on device, untimed; "
                     "reference parity-check matrix file",
+            "trial_generation_s": trial_gen_s,
             "config": {
                 "workload": desc, "matrix": fixture, "n": n, "m": m, "edges": E, "info_bits_per_frame": k_info,
                 "algorithm": Q.ALGORITHM_NAMES[alg], "qber": qber, "max_iterations": args.max_iterations,
@@ -196,7 +211,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
-                                               args.cpu_baseline_seconds, k_info)
+                                               args.cpu_baseline_seconds, k_info,
+                                               SIMULATION_SEEDS.get(args.workload, 1022025) + 1)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()
@@ -223,23 +239,25 @@ def combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, frames, kernel_ms, device
             "ok": float(stats[2]), "keys": float(stats[3]), "frames": float(stats[4])}
 
 
-def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info):
+def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info, seed):
     """The CPU oracle (a port of the reference decoder, glibc math, one frame per
     task on a thread pool like src/simulation.cpp:721,740-746) on a bounded
     sample of the same workload: chunks of frames until `seconds` elapse."""
-    import qkd_ldpc_v_amd as Q
+    from oracle import pyoracle as P
     from oracle.pyoracle import Oracle
 
     threads = max(1, min(16, os.cpu_count() or 1))
     O = Oracle(H)
     p = O.params(alg, max_it, True, 100.0, prim, sec)
     chunk = threads * 4
+    seeds = P.trial_seeds(seed, 1 << 16)
     frames = 0
     t_dec = 0.0
-    seed = 5
-    while t_dec < seconds:
-        a, b, q = Q.bsc_frames(H.n, qber, chunk, seed=seed)
-        seed += 1
+    while t_dec < seconds and frames + chunk <= seeds.size:
+        tr = [P.trial(H.n, qber, int(sd)) for sd in seeds[frames:frames + chunk]]  # run_trial's keys, untimed
+        a = np.stack([t[0] for t in tr])
+        b = np.stack([t[1] for t in tr])
+        q = tr[0][2]
         t0 = time.perf_counter()
         lp = math.log((1.0 - q) / q)
         llr = np.where(b != 0, -lp, lp)

@@ -171,6 +171,21 @@ const char *qldpc_last_error(void);
 /* Library version string. */
 const char *qldpc_version(void);
 
+/* ---- Trial generator ------------------------------------
+ * qldpc_trial_seeds: the simulation loop's per-trial seeds — `count` draws of
+ * uniform_int_distribution<size_t>(0, SIZE_MAX) over Xoshiro256PlusPlus(
+ * simulation_seed) (src/simulation.cpp:713-719).  Host only.
+ * qldpc_trials_device: for each trial f, run_trial's keys
+ * (src/simulation.cpp:540-551): Alice = fill_random_bits, Bob = inject_errors
+ * (src/array_and_matrix_operations.cpp:889-933) from a generator seeded with
+ * d_seeds[f] + seed_add (the loop's `seeds[n] + curr_sim`, :743), with
+ * libstdc++ 11's draw consumption.  d_alice/d_bob: batch*n bytes.  Returns
+ * the accurate QBER floor(n*qber)/n; QLDPC_EINVAL (the reference's "too small
+ * for QBER" error) when floor(n*qber) == 0. */
+int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_out);
+int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
+                        uint8_t *d_alice, uint8_t *d_bob, double *accurate_qber_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,10 @@ def lib():
         L.qlo_decode_trace.argtypes = [P, ctypes.POINTER(_Params), P, P, P, P, P, P]
         L.qlo_decode_batch.argtypes = [P, ctypes.POINTER(_Params), ctypes.c_int32, P, P, P, P, P, P, ctypes.c_int32]
         L.qlo_build_frame.argtypes = [P, P, P, ctypes.c_double, P, P]
+        L.qlo_xoshiro.argtypes = [ctypes.c_uint64, ctypes.c_int32, P]
+        L.qlo_trial_seeds.argtypes = [ctypes.c_uint64, ctypes.c_int32, P]
+        L.qlo_trial.restype = ctypes.c_double
+        L.qlo_trial.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_uint64, P, P]
         _lib = L
     return _lib
 
@@ -111,3 +115,24 @@ class Oracle:
         lib().qlo_decode_batch(self._g, ctypes.byref(p), batch, _p(l), _p(s), _p(out), _p(it), _p(ok), _p(post),
                                int(threads))
         return out, it, ok, post
+
+
+# ---- trial generator (trials_oracle.cpp) ------------------------------------
+def xoshiro(seed: int, count: int) -> np.ndarray:
+    out = np.empty(count, np.uint64)
+    lib().qlo_xoshiro(seed, count, out.ctypes.data)
+    return out
+
+
+def trial_seeds(simulation_seed: int, count: int) -> np.ndarray:
+    out = np.empty(count, np.uint64)
+    lib().qlo_trial_seeds(simulation_seed, count, out.ctypes.data)
+    return out
+
+
+def trial(n: int, qber: float, seed: int):
+    """-> (alice u8[n], bob u8[n], accurate_qber) as run_trial generates them."""
+    a = np.empty(n, np.uint8)
+    b = np.empty(n, np.uint8)
+    q = lib().qlo_trial(n, qber, int(seed) & 0xFFFFFFFFFFFFFFFF, a.ctypes.data, b.ctypes.data)
+    return a, b, q

@@ -6,11 +6,12 @@ this package binds it and mirrors the reference's decode interface
 """
 from ._lib import (ALGORITHM_NAMES, ANMSA, AOMSA, NMSA, OMSA, SPA, SPA_LIN, Params, QLDPCError, exported_symbols, lib,
                    log_p, version)
-from .graph import DecodeOutput, Graph, HMatrix, keys_match_device, load_matrix
+from .graph import DecodeOutput, Graph, HMatrix, keys_match_device, load_matrix, trial_seeds, trials_device
 from .trials import bsc_frames
 
 __all__ = [
     "ALGORITHM_NAMES", "ANMSA", "AOMSA", "NMSA", "OMSA", "SPA", "SPA_LIN", "Params", "QLDPCError",
     "exported_symbols", "lib", "log_p", "version", "DecodeOutput", "Graph", "HMatrix", "keys_match_device",
+    "trial_seeds", "trials_device",
     "load_matrix", "bsc_frames",
 ]

@@ -68,6 +68,9 @@ _SIGNATURES = {
         [_P, _I32, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     ),
     "qldpc_selftest_math_device": (_I32, [_I32, _I32, _P, _P, _P]),
+    "qldpc_trial_seeds": (_I32, [ctypes.c_uint64, _I32, _P]),
+    "qldpc_trials_device": (_I32, [_I32, ctypes.c_double, _I32, _P, ctypes.c_uint64, _P, _P,
+                                   ctypes.POINTER(ctypes.c_double), _P]),
     "qldpc_last_error": (ctypes.c_char_p, []),
     "qldpc_version": (ctypes.c_char_p, []),
 }

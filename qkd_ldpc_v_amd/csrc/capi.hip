@@ -883,4 +883,54 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
     return rc;
 }
 
+// ---- trial generator (src/simulation.cpp:540-551,713-719,743) ----------------
+int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_out) {
+    if (count < 0 || (count > 0 && !seeds_out)) return fail(QLDPC_EINVAL, "bad count / NULL seeds_out");
+    // Xoshiro256++ seeded by four SplitMix64 outputs (Xoshiro-cpp); the
+    // reference draws seeds with uniform_int_distribution<size_t>(0, SIZE_MAX),
+    // which passes each 64-bit output through unchanged.
+    uint64_t st[4], x = simulation_seed;
+    for (auto &v : st) {
+        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        v = z ^ (z >> 31);
+    }
+    auto rotl = [](uint64_t v, int k) { return (v << k) | (v >> (64 - k)); };
+    for (int32_t i = 0; i < count; ++i) {
+        seeds_out[i] = rotl(st[0] + st[3], 23) + st[0];
+        const uint64_t t = st[1] << 17;
+        st[2] ^= st[0];
+        st[3] ^= st[1];
+        st[1] ^= st[2];
+        st[0] ^= st[3];
+        st[2] ^= t;
+        st[3] = rotl(st[3], 45);
+    }
+    return QLDPC_OK;
+}
+
+int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
+                        uint8_t *d_alice, uint8_t *d_bob, double *accurate_qber_out, void *stream) {
+    if (n <= 0 || batch < 0) return fail(QLDPC_EINVAL, "n must be > 0 and batch >= 0");
+    const uint64_t n_err = (uint64_t)((double)n * qber);
+    if (n_err == 0)  // run_trial's own check (src/simulation.cpp:552-553)
+        return fail(QLDPC_EINVAL, "Key size '" + std::to_string(n) + "' is too small for QBER.");
+    if (n_err > (uint64_t)n) return fail(QLDPC_EINVAL, "QBER must be <= 1");
+    if (accurate_qber_out) *accurate_qber_out = (double)n_err / (double)n;
+    if (batch == 0) return QLDPC_OK;
+    if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
+    const hipStream_t s = (hipStream_t)stream;
+    uint32_t *scratch = nullptr;
+    const size_t words = trials_scratch_words(n, batch);
+    if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
+    hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, s);
+    if (scratch) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(scratch);
+    }
+    if (e != hipSuccess) return hip_fail(e, "trials");
+    return QLDPC_OK;
+}
+
 }  // extern "C"

@@ -112,6 +112,10 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 hipError_t occupancy_v2(int R, int RG, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
                             uint8_t *pal_ok, hipStream_t stream);
+size_t trials_lds_bytes(int n);
+size_t trials_scratch_words(int n, int batch);
+hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
+                         uint8_t *bob, uint32_t *scratch, hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
                              uint8_t *match, hipStream_t stream);

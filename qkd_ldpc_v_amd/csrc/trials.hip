@@ -1,0 +1,176 @@
+// trials.hip — the reference's trial generator on device.
+//
+// Per trial f (src/simulation.cpp:540-551): a Xoshiro256++ generator seeded
+// with seeds[f] + seed_add (the simulation loop's `seeds[n] + curr_sim`,
+// :743), Alice's key from uniform_int_distribution<int>(0, 1) draws
+// (fill_random_bits, src/array_and_matrix_operations.cpp:889-901), Bob's key
+// with exactly floor(n*QBER) errors at the first positions of a std::shuffle'd
+// index vector (inject_errors, :904-933).  Draw consumption follows libstdc++
+// 11 exactly: uniform_int_distribution downscales a 64-bit generator with
+// Lemire's nearly-divisionless method (_S_nd over unsigned __int128), and
+// std::shuffle takes the two-swaps-per-draw path (__gen_two_uniform_ints)
+// because (2^64-1)/n >= n.
+//
+// Fisher-Yates is sequential, so one lane per trial runs it; the index vector
+// lives in LDS (uint16) for n <= 65536, in global scratch (uint32) above.
+// Many trials run concurrently (one 64-lane workgroup each); the other lanes
+// initialise the index vector and write the keys out coalesced.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qldpc {
+namespace {
+
+struct Xoshiro256pp {
+    uint64_t s0, s1, s2, s3;
+    __device__ static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    __device__ explicit Xoshiro256pp(uint64_t seed) {  // Xoshiro-cpp: four SplitMix64 outputs
+        uint64_t x = seed;
+        uint64_t *st[4] = {&s0, &s1, &s2, &s3};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            *st[i] = z ^ (z >> 31);
+        }
+    }
+    __device__ uint64_t next() {
+        const uint64_t r = rotl(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 45);
+        return r;
+    }
+};
+
+// libstdc++ uniform_int_distribution::_S_nd<unsigned __int128>: a value in
+// [0, range) from a 64-bit generator.
+__device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
+    uint64_t x = g.next();
+    uint64_t lo = x * range;
+    uint64_t hi = __umul64hi(x, range);
+    if (lo < range) {
+        const uint64_t threshold = (0 - range) % range;
+        while (lo < threshold) {
+            x = g.next();
+            lo = x * range;
+            hi = __umul64hi(x, range);
+        }
+    }
+    return hi;
+}
+
+template <typename IDX, bool IN_LDS>
+__global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
+                                                    uint64_t seed_add, uint8_t *alice, uint8_t *bob,
+                                                    uint32_t *scratch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int f = blockIdx.x;
+    if (f >= batch) return;
+    const int words = (n + 31) / 32;
+    uint32_t *abits = reinterpret_cast<uint32_t *>(smem);
+    uint32_t *flips = abits + words;
+    IDX *perm = IN_LDS ? reinterpret_cast<IDX *>(flips + words)
+                       : reinterpret_cast<IDX *>(scratch + (size_t)blockIdx.x * (size_t)n);
+    const int lane = threadIdx.x;
+    for (int i = lane; i < words; i += 64) {
+        abits[i] = 0;
+        flips[i] = 0;
+    }
+    if (n_err > 0)
+        for (int i = lane; i < n; i += 64) perm[i] = (IDX)i;
+    __syncthreads();
+    if (lane == 0) {
+        Xoshiro256pp g(seeds[f] + seed_add);
+        // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
+        // which never rejects: the top bit of each draw.
+        for (int w = 0; w < words; ++w) {
+            uint32_t v = 0;
+            const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
+            for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
+            abits[w] = v;
+        }
+        if (n_err > 0) {
+            // std::shuffle(first, last, g), libstdc++ 11 (bits/stl_algo.h)
+            uint64_t i = 1;
+            if ((n & 1) == 0) {
+                const uint64_t d = draw_below(g, 2);
+                const IDX t = perm[1];
+                perm[1] = perm[d];
+                perm[d] = t;
+                i = 2;
+            }
+            while (i != (uint64_t)n) {
+                const uint64_t b0 = i + 1, b1 = i + 2;  // __gen_two_uniform_ints(b0, b0 + 1)
+                const uint64_t x = draw_below(g, b0 * b1);
+                uint64_t p1, p2;
+                if (x < 0x100000000ull) {  // 32-bit divide when it fits (n <= 65535 always)
+                    const uint32_t x32 = (uint32_t)x, d32 = (uint32_t)b1;
+                    p1 = x32 / d32;
+                    p2 = x32 - (uint32_t)p1 * d32;
+                } else {
+                    p1 = x / b1;
+                    p2 = x % b1;
+                }
+                IDX t = perm[i];
+                perm[i] = perm[p1];
+                perm[p1] = t;
+                t = perm[i + 1];
+                perm[i + 1] = perm[p2];
+                perm[p2] = t;
+                i += 2;
+            }
+            for (uint64_t e = 0; e < n_err; ++e) {
+                const uint32_t p = (uint32_t)perm[e];
+                flips[p >> 5] |= 1u << (p & 31);
+            }
+        }
+    }
+    __syncthreads();
+    uint8_t *a = alice + (size_t)f * n;
+    uint8_t *b = bob + (size_t)f * n;
+    for (int i = lane; i < n; i += 64) {
+        const uint32_t av = (abits[i >> 5] >> (i & 31)) & 1u;
+        const uint32_t fv = (flips[i >> 5] >> (i & 31)) & 1u;
+        a[i] = (uint8_t)av;
+        b[i] = (uint8_t)(av ^ fv);
+    }
+}
+
+}  // namespace
+
+size_t trials_lds_bytes(int n) {
+    const size_t words = (size_t)(n + 31) / 32;
+    return 8 * words + (n <= 65536 ? 2 * (size_t)n : 0);
+}
+
+size_t trials_scratch_words(int n, int batch) { return n <= 65536 ? 0 : (size_t)n * (size_t)batch; }
+
+hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
+                         uint8_t *bob, uint32_t *scratch, hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    const size_t lds = trials_lds_bytes(n);
+    if (n <= 65536) {
+        auto k = trials_kernel<uint16_t, true>;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
+                           scratch);
+    } else {
+        auto k = trials_kernel<uint32_t, false>;
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
+                           scratch);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace qldpc

@@ -184,6 +184,28 @@ def keys_match_device(alice, bits, out, stream=None) -> None:
                                         out.data_ptr(), _stream_ptr(stream, dev)), "qldpc_keys_match_device")
 
 
+def trial_seeds(simulation_seed: int, count: int) -> np.ndarray:
+    """Per-trial seeds of the simulation loop (src/simulation.cpp:713-719)."""
+    out = np.empty(count, np.uint64)
+    check(lib().qldpc_trial_seeds(int(simulation_seed) & 0xFFFFFFFFFFFFFFFF, int(count), out.ctypes.data),
+          "qldpc_trial_seeds")
+    return out
+
+
+def trials_device(n: int, qber: float, seeds, alice, bob, seed_add: int = 0, stream=None) -> float:
+    """run_trial's keys for every seed, on device (src/simulation.cpp:540-551).
+    seeds: device uint64 tensor [batch]; alice/bob: device uint8 [batch, n].
+    Returns the accurate QBER floor(n*qber)/n."""
+    import ctypes
+
+    dev = seeds.device.index
+    q = ctypes.c_double(0.0)
+    check(lib().qldpc_trials_device(int(n), float(qber), int(seeds.shape[0]), seeds.data_ptr(),
+                                    int(seed_add) & 0xFFFFFFFFFFFFFFFF, alice.data_ptr(), bob.data_ptr(),
+                                    ctypes.byref(q), _stream_ptr(stream, dev)), "qldpc_trials_device")
+    return q.value
+
+
 def _stream_ptr(stream, device: int):
     if stream is None:
         import torch

@@ -1,0 +1,117 @@
+"""Trial generator: the reference's run_trial keys.
+
+CPU: the oracle's generator (libstdc++'s own uniform_int_distribution and
+std::shuffle over a restated Xoshiro256++) against an independent pure-Python
+restatement of the same algorithms, and the product's host seed sequence
+against the oracle.  GPU: qldpc_trials_device against the oracle, bit for bit.
+Upstream Xoshiro-cpp is not in the image: the generator itself is parity
+unpinned against it (published algorithm, SplitMix64 seeding)."""
+import numpy as np
+import pytest
+
+import qkd_ldpc_v_amd as Q
+from oracle import pyoracle as P
+
+M64 = (1 << 64) - 1
+
+
+class PyXoshiro:
+    def __init__(self, seed):
+        x = seed & M64
+        self.s = []
+        for _ in range(4):
+            x = (x + 0x9E3779B97F4A7C15) & M64
+            z = x
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+            self.s.append(z ^ (z >> 31))
+
+    @staticmethod
+    def rotl(v, k):
+        return ((v << k) | (v >> (64 - k))) & M64
+
+    def __call__(self):
+        s = self.s
+        r = (self.rotl((s[0] + s[3]) & M64, 23) + s[0]) & M64
+        t = (s[1] << 17) & M64
+        s[2] ^= s[0]
+        s[3] ^= s[1]
+        s[1] ^= s[2]
+        s[0] ^= s[3]
+        s[2] ^= t
+        s[3] = self.rotl(s[3], 45)
+        return r
+
+
+def py_below(g, rng):  # libstdc++ _S_nd<unsigned __int128>
+    p = g() * rng
+    lo = p & M64
+    if lo < rng:
+        thr = ((1 << 64) - rng) % rng
+        while lo < thr:
+            p = g() * rng
+            lo = p & M64
+    return p >> 64
+
+
+def py_trial(n, qber, seed):
+    g = PyXoshiro(seed)
+    a = [py_below(g, 2) for _ in range(n)]
+    ne = int(float(n) * qber)
+    b = list(a)
+    pos = list(range(n))
+    i = 1
+    if n % 2 == 0:
+        d = py_below(g, 2)
+        pos[1], pos[d] = pos[d], pos[1]
+        i = 2
+    while i != n:
+        b0 = i + 1
+        x = py_below(g, b0 * (b0 + 1))
+        p1, p2 = x // (b0 + 1), x % (b0 + 1)
+        pos[i], pos[p1] = pos[p1], pos[i]
+        pos[i + 1], pos[p2] = pos[p2], pos[i + 1]
+        i += 2
+    for e in range(ne):
+        b[pos[e]] ^= 1
+    return np.array(a, np.uint8), np.array(b, np.uint8), ne / n
+
+
+@pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (10240, 0.013, 1022025)])
+def test_oracle_trial_matches_python_restatement(n, qber, seed):
+    a, b, q = P.trial(n, qber, seed)
+    pa, pb, pq = py_trial(n, qber, seed)
+    assert np.array_equal(a, pa) and np.array_equal(b, pb) and q == pq
+    assert int((a != b).sum()) == int(n * qber)
+
+
+def test_seed_sequences_agree():
+    g = PyXoshiro(1022025)
+    want = np.array([g() for _ in range(16)], np.uint64)
+    assert np.array_equal(P.trial_seeds(1022025, 16), want)
+    assert np.array_equal(P.xoshiro(1022025, 16), want)
+    assert np.array_equal(Q.trial_seeds(1022025, 16), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,qber", [(1024, 0.013), (10240, 0.0215), (10241, 0.05), (102400, 0.038)])
+def test_device_trials_bitexact(gpu_available, n, qber):
+    import torch
+
+    batch = 24 if n < 100000 else 4
+    seeds = Q.trial_seeds(9012025, batch)
+    d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()
+    da = torch.empty((batch, n), dtype=torch.uint8, device="cuda")
+    db = torch.empty_like(da)
+    q = Q.trials_device(n, qber, d_seeds, da, db, seed_add=3)
+    torch.cuda.synchronize()
+    A, B = da.cpu().numpy(), db.cpu().numpy()
+    for f in range(batch):
+        a, b, qo = P.trial(n, qber, (int(seeds[f]) + 3) & M64)
+        assert np.array_equal(A[f], a) and np.array_equal(B[f], b), f"trial {f} differs"
+        assert q == qo
+
+
+def test_too_small_for_qber_is_an_error():
+    with pytest.raises(Q.QLDPCError, match="too small for QBER"):
+        Q._lib.check(Q.lib().qldpc_trials_device(10, 0.01, 0, None, 0, None, None, None, None), "trials")
