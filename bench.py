@@ -40,11 +40,15 @@ WORKLOADS = {
     "c5": ("c5_n10240_m2048.sp2", 3, 5, 0.7, 0.99, 0.0156, 4096,
            "C5 decode: n=10k R=0.8 irregular (matrices_2, format 3) AOMSA beta=0.7 sigma=0.99 "
            "(configs/ADAPTIVE T.json, rate bucket 0.805) 50-iter, QBER 1.56%, batch 4096/GPU, no rate adaptation"),
+    "c5ra": ("c5_n10240_m2048.sp2", 3, 5, 0.7, 0.99, 0.0156, 4096,
+             "C5: n=10k R=0.8 irregular, rate-adapted (untainted puncturing, QBER 1.56%, delta 0.06, f_EC 1.39 -> "
+             "configs/ADAPTIVE T.json), AOMSA beta=0.7 sigma=0.99 50-iter, batch 4096/GPU"),
 }
 
 
 # SIMULATION_SEED of the config each workload comes from (configs_all/*.json).
 SIMULATION_SEEDS = {"c1": 9012025, "c2": 1022025, "c3": 10022025}
+RATE_ADAPT = {"c5ra": (0.06, 1.39, "c5_n10240_m2048.untp")}  # delta, efficiency, untainted list
 
 
 def log(*a):
@@ -94,13 +98,30 @@ def main():
     # The reference's generator (src/simulation.cpp:540-551,713-719,743):
     # per-trial seeds drawn from Xoshiro256++(SIMULATION_SEED); each rank takes
     # its own contiguous slice of trials.
-    seeds = Q.trial_seeds(SIMULATION_SEEDS.get(args.workload, 1022025), batch * world)[rank * batch:(rank + 1) * batch]
+    sim_seed = SIMULATION_SEEDS.get(args.workload, 1022025)
+    seeds = Q.trial_seeds(sim_seed, batch * world)[rank * batch:(rank + 1) * batch]
     d_seeds = torch.from_numpy(seeds.view(np.int64)).to(dev)
     ta = torch.empty((batch, n), dtype=torch.uint8, device=dev)
     tb = torch.empty((batch, n), dtype=torch.uint8, device=dev)
+    ra = RATE_ADAPT.get(args.workload)
+    if ra:  # adapt_code_rate on the host, then the rate-adapted trials
+        import gzip
+
+        untp = np.array(gzip.open(os.path.join(ROOT, "tests", "golden", "matrices", ra[2] + ".gz")).read().split(),
+                        np.int32)
+        punct, short, rate = Q.adapt_code_rate(n, m, qber, ra[0], ra[1], untp, Q.xoshiro_state(sim_seed))
+        rplan = g.rate_plan(punct, short)
+        pa = torch.empty((batch, max(1, punct.size)), dtype=torch.uint8, device=dev)
+        pb = torch.empty_like(pa)
+        tax = torch.empty((batch, n), dtype=torch.uint8, device=dev)  # Alice's extended key
+        k_info = n - m - short.size  # information bits of the adapted code
+        desc += f" [p={punct.size} s={short.size} R={rate:.4f}]"
     torch.cuda.synchronize()
     tg0 = time.perf_counter()
-    q_acc = Q.trials_device(n, qber, d_seeds, ta, tb)
+    if ra:
+        q_acc = Q.trials_rate_adapt_device(n, qber, d_seeds, punct.size, ta, tb, pa, pb)
+    else:
+        q_acc = Q.trials_device(n, qber, d_seeds, ta, tb)
     torch.cuda.synchronize()
     trial_gen_s = time.perf_counter() - tg0
     lp = Q.log_p(q_acc)
@@ -125,13 +146,16 @@ def main():
     def step(i, timed=False):
         sl = slots[i % nst]
         st = sl.stream
-        g.build_frames_device(ta, tb, tlp, sl.llr_ws, sl.syn_ws, stream=st)
+        if ra:  # QKD_LDPC_RATE_ADAPT (src/qkd_ldpc_algorithm.cpp:1121-1218)
+            g.build_frames_rate_adapt_device(rplan, ta, tb, pa, pb, tlp, tax, sl.llr_ws, sl.syn_ws, stream=st)
+        else:  # QKD_LDPC (:1031-1087)
+            g.build_frames_device(ta, tb, tlp, sl.llr_ws, sl.syn_ws, stream=st)
         if timed:
             ev0[i].record(st)
         g.decode_device(params, sl.llr_ws, sl.syn_ws, sl.bits, sl.iters, sl.ok, stream=st)
         if timed:
             ev1[i].record(st)
-        Q.keys_match_device(ta, sl.bits, sl.km, stream=st)
+        Q.keys_match_device(tax if ra else ta, sl.bits, sl.km, stream=st)
 
     log(f"[rank {rank}] {desc}; plan {plan}; warmup {args.warmup}")
     for i in range(args.warmup):

@@ -186,6 +186,50 @@ int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_o
 int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
                         uint8_t *d_alice, uint8_t *d_bob, double *accurate_qber_out, void *stream);
 
+/* ---- Rate adaptation (a15) -----------------------------
+ * qldpc_xoshiro_state: the 4-word state of Xoshiro256PlusPlus(seed).
+ * qldpc_adapt_code_rate: adapt_code_rate (src/array_and_matrix_operations.cpp:
+ * 1131-1223): numbers and ascending positions of punctured / shortened bits
+ * for (qber, delta, efficiency), drawing from the generator whose state is
+ * prng_state (advanced in place, so successive calls chain like the
+ * reference's setup loop, src/simulation.cpp:394-455).  Untainted puncturing
+ * takes the first positions of the .untp list.  Out-of-range combinations
+ * (the reference's WARNING + skip) return QLDPC_OK with zero counts.
+ * punctured_out / shortened_out need capacity n (NULL: counts only).
+ * qldpc_rate_plan_create: the position classes of one (punctured, shortened)
+ * pair, replicated on the graph's devices.
+ * qldpc_trials_rate_adapt_device: qldpc_trials_device plus, per trial, the
+ * 2 * n_punct further draws QKD_LDPC_RATE_ADAPT takes for punctured positions
+ * (src/qkd_ldpc_algorithm.cpp:1148-1157) -> d_punct_alice/bob [batch*n_punct].
+ * qldpc_build_frames_rate_adapt_device: the extended frame (:1141-1180):
+ * Alice's extended key [batch*n], LLRs (+-log_p / 1e-4 / DBL_MAX) [batch*n]
+ * and Alice's syndrome [batch*m].
+ * qldpc_qkd_ldpc_rate_adapt_batch_device: QKD_LDPC_RATE_ADAPT's window on
+ * device: frame build + decode + keys_match against the extended key (:1216). */
+typedef struct qldpc_rate_plan qldpc_rate_plan;
+int qldpc_xoshiro_state(uint64_t seed, uint64_t *state_out);
+int qldpc_adapt_code_rate(int32_t n, int32_t m, double qber, double delta, double efficiency,
+                          int32_t untainted_enabled, const int32_t *untainted, int32_t n_untainted,
+                          uint64_t *prng_state, int32_t *punctured_out, int32_t *n_punctured, int32_t *shortened_out,
+                          int32_t *n_shortened, double *adapted_rate_out);
+int qldpc_rate_plan_create(qldpc_graph *g, int32_t n_punct, const int32_t *punctured, int32_t n_short,
+                           const int32_t *shortened, qldpc_rate_plan **out);
+void qldpc_rate_plan_destroy(qldpc_rate_plan *plan);
+int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
+                                   int32_t n_punct, uint8_t *d_alice, uint8_t *d_bob, uint8_t *d_punct_alice,
+                                   uint8_t *d_punct_bob, double *accurate_qber_out, void *stream);
+int qldpc_build_frames_rate_adapt_device(qldpc_graph *g, const qldpc_rate_plan *plan, int32_t device, int32_t batch,
+                                         const uint8_t *d_alice, const uint8_t *d_bob, const uint8_t *d_punct_alice,
+                                         const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext,
+                                         double *d_llr, uint8_t *d_syndrome, void *stream);
+int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan *plan, int32_t device,
+                                           const qldpc_params *p, int32_t batch, const uint8_t *d_alice,
+                                           const uint8_t *d_bob, const uint8_t *d_punct_alice,
+                                           const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext,
+                                           double *d_llr_ws, uint8_t *d_synd_ws, uint8_t *d_bits_out,
+                                           uint32_t *d_iters_out, uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out,
+                                           void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,13 @@ def lib():
         L.qlo_trial_seeds.argtypes = [ctypes.c_uint64, ctypes.c_int32, P]
         L.qlo_trial.restype = ctypes.c_double
         L.qlo_trial.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_uint64, P, P]
+        L.qlo_adapt_code_rate.restype = ctypes.c_int32
+        L.qlo_adapt_code_rate.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                          ctypes.c_double, ctypes.c_int32, P, ctypes.c_int32, P, P,
+                                          ctypes.POINTER(ctypes.c_int32), P, ctypes.POINTER(ctypes.c_int32)]
+        L.qlo_trial_rate_adapt.restype = ctypes.c_double
+        L.qlo_trial_rate_adapt.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_uint64, ctypes.c_int32, P,
+                                           ctypes.c_int32, P, P, P]
         _lib = L
     return _lib
 
@@ -136,3 +143,26 @@ def trial(n: int, qber: float, seed: int):
     b = np.empty(n, np.uint8)
     q = lib().qlo_trial(n, qber, int(seed) & 0xFFFFFFFFFFFFFFFF, a.ctypes.data, b.ctypes.data)
     return a, b, q
+
+
+def adapt_code_rate(n, m, qber, delta, efficiency, untainted, state):
+    """-> (punctured, shortened) and advances `state` (np.uint64[4]) in place."""
+    unt = None if untainted is None else np.ascontiguousarray(untainted, np.int32)
+    p = np.empty(n, np.int32)
+    s = np.empty(n, np.int32)
+    npn, nsn = ctypes.c_int32(0), ctypes.c_int32(0)
+    lib().qlo_adapt_code_rate(n, m, qber, delta, efficiency, 0 if unt is None else 1, _p(unt),
+                              0 if unt is None else unt.size, state.ctypes.data, p.ctypes.data, ctypes.byref(npn),
+                              s.ctypes.data, ctypes.byref(nsn))
+    return p[:npn.value].copy(), s[:nsn.value].copy()
+
+
+def trial_rate_adapt(n, qber, seed, punct, short):
+    """-> (alice_ext u8[n], llr f64[n], accurate_qber) of QKD_LDPC_RATE_ADAPT."""
+    pa = np.ascontiguousarray(punct, np.int32)
+    sh = np.ascontiguousarray(short, np.int32)
+    a = np.empty(n, np.uint8)
+    llr = np.empty(n, np.float64)
+    q = lib().qlo_trial_rate_adapt(n, qber, int(seed) & 0xFFFFFFFFFFFFFFFF, pa.size, pa.ctypes.data, sh.size,
+                                   sh.ctypes.data, a.ctypes.data, llr.ctypes.data)
+    return a, llr, q

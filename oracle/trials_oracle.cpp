@@ -15,6 +15,7 @@
 // Xoshiro-cpp v1.1's seeding (four SplitMix64 outputs), which is absent from
 // this image: that part is "parity unpinned" against the upstream header.
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <limits>
@@ -88,6 +89,86 @@ double qlo_trial(int32_t n, double qber, uint64_t seed, uint8_t *alice, uint8_t 
         bob[i] = (uint8_t)b[i];
     }
     return static_cast<double>(ne) / static_cast<double>(n);
+}
+
+}  // extern "C"
+
+// ---- rate adaptation (src/array_and_matrix_operations.cpp:1131-1223;
+//      src/qkd_ldpc_algorithm.cpp:1121-1180) ---------------------------------
+extern "C" {
+
+// adapt_code_rate over a generator whose 4-word state is advanced in place.
+// Returns 0 and counts (0/0 for the reference's skipped combinations).
+int qlo_adapt_code_rate(int32_t n, int32_t m, double qber, double delta, double efficiency, int32_t untainted_on,
+                        const int32_t *untainted, int32_t n_untainted, uint64_t *state, int32_t *punct,
+                        int32_t *n_punct, int32_t *shortened, int32_t *n_short) {
+    Xoshiro256pp g(0);
+    std::memcpy(g.s, state, sizeof g.s);
+    *n_punct = *n_short = 0;
+    const double h_b = -qber * std::log2(qber) - (1. - qber) * std::log2(1. - qber);
+    const double optimal_R = 1. - efficiency * h_b;
+    const double original_R = 1. - static_cast<double>(m) / static_cast<double>(n);
+    const int ns = static_cast<int>(std::ceil((original_R - optimal_R * (1. - delta)) * static_cast<double>(n)));
+    const int np = static_cast<int>(delta * static_cast<double>(n) - static_cast<double>(ns));
+    if (ns <= 0 || np <= 0) return 0;
+    std::vector<int> p, pos(n);
+    if (untainted_on) {
+        if (np > n_untainted) return 0;
+        p.assign(untainted, untainted + np);
+    } else {
+        for (int i = 0; i < n; ++i) pos[i] = i;
+        std::shuffle(pos.begin(), pos.end(), g);
+        p.assign(pos.begin(), pos.begin() + np);
+    }
+    std::sort(p.begin(), p.end());
+    for (int i = 0; i < n; ++i) pos[i] = i;
+    std::vector<int> rem(n - np);
+    std::set_difference(pos.begin(), pos.end(), p.begin(), p.end(), rem.begin());
+    std::shuffle(rem.begin(), rem.end(), g);
+    std::vector<int> s(rem.begin(), rem.begin() + ns);
+    std::sort(s.begin(), s.end());
+    std::memcpy(state, g.s, sizeof g.s);
+    std::copy(p.begin(), p.end(), punct);
+    std::copy(s.begin(), s.end(), shortened);
+    *n_punct = np;
+    *n_short = ns;
+    return 0;
+}
+
+// A rate-adapted trial: run_trial's keys, then QKD_LDPC_RATE_ADAPT's extended
+// frame.  Outputs alice_ext[n], llr[n]; returns the accurate QBER.
+double qlo_trial_rate_adapt(int32_t n, double qber, uint64_t seed, int32_t n_punct, const int32_t *punct,
+                            int32_t n_short, const int32_t *shortened, uint8_t *alice_ext, double *llr) {
+    Xoshiro256pp g(seed);
+    std::vector<int> a(n), b;
+    std::uniform_int_distribution<int> bit(0, 1);
+    for (int32_t i = 0; i < n; ++i) a[i] = bit(g);
+    const size_t ne = static_cast<size_t>(static_cast<double>(n) * qber);
+    b = a;
+    std::vector<size_t> pos(n);
+    for (int32_t i = 0; i < n; ++i) pos[i] = (size_t)i;
+    std::shuffle(pos.begin(), pos.end(), g);
+    for (size_t i = 0; i < ne; ++i) b[pos[i]] ^= 1;
+    const double q = static_cast<double>(ne) / static_cast<double>(n);
+    const double log_p = std::log((1. - q) / q);
+    int p = 0, s = 0, k = 0;
+    for (int i = 0; i < n; ++i) {
+        if (p < n_punct && punct[p] == i) {
+            alice_ext[i] = (uint8_t)bit(g);
+            (void)bit(g);  // Bob's punctured bit
+            llr[i] = 1e-4;
+            ++p;
+        } else if (s < n_short && shortened[s] == i) {
+            alice_ext[i] = 0;
+            llr[i] = std::numeric_limits<double>::max();
+            ++s;
+        } else {
+            alice_ext[i] = (uint8_t)a[k];
+            llr[i] = b[k] ? -log_p : log_p;
+            ++k;
+        }
+    }
+    return q;
 }
 
 }  // extern "C"

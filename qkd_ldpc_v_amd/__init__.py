@@ -6,12 +6,13 @@ this package binds it and mirrors the reference's decode interface
 """
 from ._lib import (ALGORITHM_NAMES, ANMSA, AOMSA, NMSA, OMSA, SPA, SPA_LIN, Params, QLDPCError, exported_symbols, lib,
                    log_p, version)
-from .graph import DecodeOutput, Graph, HMatrix, keys_match_device, load_matrix, trial_seeds, trials_device
+from .graph import (DecodeOutput, Graph, HMatrix, RatePlan, adapt_code_rate, keys_match_device, load_matrix,
+                    trial_seeds, trials_device, trials_rate_adapt_device, xoshiro_state)
 from .trials import bsc_frames
 
 __all__ = [
     "ALGORITHM_NAMES", "ANMSA", "AOMSA", "NMSA", "OMSA", "SPA", "SPA_LIN", "Params", "QLDPCError",
     "exported_symbols", "lib", "log_p", "version", "DecodeOutput", "Graph", "HMatrix", "keys_match_device",
-    "trial_seeds", "trials_device",
+    "trial_seeds", "trials_device", "RatePlan", "adapt_code_rate", "trials_rate_adapt_device", "xoshiro_state",
     "load_matrix", "bsc_frames",
 ]

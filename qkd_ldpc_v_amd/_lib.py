@@ -69,6 +69,16 @@ _SIGNATURES = {
     ),
     "qldpc_selftest_math_device": (_I32, [_I32, _I32, _P, _P, _P]),
     "qldpc_trial_seeds": (_I32, [ctypes.c_uint64, _I32, _P]),
+    "qldpc_xoshiro_state": (_I32, [ctypes.c_uint64, _P]),
+    "qldpc_adapt_code_rate": (_I32, [_I32, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double, _I32, _P, _I32,
+                                     _P, _P, _PI32, _P, _PI32, ctypes.POINTER(ctypes.c_double)]),
+    "qldpc_rate_plan_create": (_I32, [_P, _I32, _P, _I32, _P, ctypes.POINTER(_P)]),
+    "qldpc_rate_plan_destroy": (None, [_P]),
+    "qldpc_trials_rate_adapt_device": (_I32, [_I32, ctypes.c_double, _I32, _P, ctypes.c_uint64, _I32, _P, _P, _P,
+                                              _P, ctypes.POINTER(ctypes.c_double), _P]),
+    "qldpc_build_frames_rate_adapt_device": (_I32, [_P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "qldpc_qkd_ldpc_rate_adapt_batch_device": (_I32, [_P, _P, _I32, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P,
+                                                      _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "qldpc_trials_device": (_I32, [_I32, ctypes.c_double, _I32, _P, ctypes.c_uint64, _P, _P,
                                    ctypes.POINTER(ctypes.c_double), _P]),
     "qldpc_last_error": (ctypes.c_char_p, []),

@@ -15,7 +15,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
+#include <random>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -83,6 +85,51 @@ struct DeviceGraph {
     int occ[6] = {0, 0, 0, 0, 0, 0};
 };
 
+}  // namespace
+
+// Rate-adaptation plan: per position its class (0 key, 1 punctured, 2
+// shortened) and source index, replicated on the graph's devices.
+struct qldpc_rate_plan {
+    struct Dev {
+        int device;
+        uint8_t *cls;
+        int32_t *src;
+    };
+    int n_punct = 0, n_short = 0;
+    std::vector<Dev> devs;
+};
+
+namespace {
+// Xoshiro256++ (Blackman & Vigna) with Xoshiro-cpp v1.1's seeding (four
+// SplitMix64 outputs) — a UniformRandomBitGenerator, so std::shuffle /
+// std::uniform_int_distribution consume it exactly as the reference does.
+struct Xoshiro256pp {
+    using result_type = uint64_t;
+    uint64_t s[4];
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    explicit Xoshiro256pp(uint64_t seed) {
+        uint64_t x = seed;
+        for (auto &v : s) {
+            uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            v = z ^ (z >> 31);
+        }
+    }
+    static constexpr result_type min() { return 0; }
+    static constexpr result_type max() { return ~(uint64_t)0; }
+    result_type operator()() {
+        const uint64_t r = rotl(s[0] + s[3], 23) + s[0];
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+};
 }  // namespace
 
 struct qldpc_graph {
@@ -883,30 +930,220 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
     return rc;
 }
 
+// ---- rate adaptation (src/array_and_matrix_operations.cpp:1131-1223) ----------
+int qldpc_xoshiro_state(uint64_t seed, uint64_t *state_out) {
+    if (!state_out) return fail(QLDPC_EINVAL, "NULL state_out");
+    Xoshiro256pp g(seed);
+    for (int i = 0; i < 4; ++i) state_out[i] = g.s[i];
+    return QLDPC_OK;
+}
+
+int qldpc_adapt_code_rate(int32_t n, int32_t m, double qber, double delta, double efficiency,
+                          int32_t untainted_enabled, const int32_t *untainted, int32_t n_untainted,
+                          uint64_t *prng_state, int32_t *punctured_out, int32_t *n_punctured, int32_t *shortened_out,
+                          int32_t *n_shortened, double *adapted_rate_out) {
+    if (n <= 0 || m < 0 || m >= n || !prng_state || !n_punctured || !n_shortened)
+        return fail(QLDPC_EINVAL, "bad dimensions or NULL outputs");
+    if (untainted_enabled && n_untainted > 0 && !untainted) return fail(QLDPC_EINVAL, "NULL untainted list");
+    *n_punctured = 0;
+    *n_shortened = 0;
+    if (adapted_rate_out) *adapted_rate_out = 0.;
+    Xoshiro256pp g(0);
+    for (int i = 0; i < 4; ++i) g.s[i] = prng_state[i];
+    const double h_b = -qber * std::log2(qber) - (1. - qber) * std::log2(1. - qber);
+    const double optimal_R = 1. - efficiency * h_b;
+    const double original_R = 1. - static_cast<double>(m) / static_cast<double>(n);
+    const int num_short = static_cast<int>(std::ceil((original_R - optimal_R * (1. - delta)) * static_cast<double>(n)));
+    const int num_punct = static_cast<int>(delta * static_cast<double>(n) - static_cast<double>(num_short));
+    // beyond the achievable range: the reference warns and skips the combination
+    if (num_short <= 0 || num_punct <= 0) return QLDPC_OK;
+    std::vector<int> punct, bit_positions(n);
+    if (untainted_enabled) {
+        if (num_punct > n_untainted) return QLDPC_OK;
+        punct.assign(untainted, untainted + num_punct);
+    } else {
+        for (int i = 0; i < n; ++i) bit_positions[i] = i;
+        std::shuffle(bit_positions.begin(), bit_positions.end(), g);
+        punct.assign(bit_positions.begin(), bit_positions.begin() + num_punct);
+    }
+    std::sort(punct.begin(), punct.end());
+    for (int i = 0; i < n; ++i) bit_positions[i] = i;
+    std::vector<int> remaining(n - num_punct);
+    std::set_difference(bit_positions.begin(), bit_positions.end(), punct.begin(), punct.end(), remaining.begin());
+    std::shuffle(remaining.begin(), remaining.end(), g);
+    std::vector<int> shortened(remaining.begin(), remaining.begin() + num_short);
+    std::sort(shortened.begin(), shortened.end());
+    for (int i = 0; i < 4; ++i) prng_state[i] = g.s[i];
+    *n_punctured = num_punct;
+    *n_shortened = num_short;
+    if (punctured_out) std::copy(punct.begin(), punct.end(), punctured_out);
+    if (shortened_out) std::copy(shortened.begin(), shortened.end(), shortened_out);
+    if (adapted_rate_out)
+        *adapted_rate_out = static_cast<double>(n - m - num_short) / static_cast<double>(n - num_punct - num_short);
+    return QLDPC_OK;
+}
+
+int qldpc_rate_plan_create(qldpc_graph *g, int32_t n_punct, const int32_t *punctured, int32_t n_short,
+                           const int32_t *shortened, qldpc_rate_plan **out) {
+    if (!g || !out) return fail(QLDPC_EINVAL, "graph / out is NULL");
+    *out = nullptr;
+    if (n_punct < 0 || n_short < 0 || n_punct + n_short > g->n || (n_punct && !punctured) || (n_short && !shortened))
+        return fail(QLDPC_EINVAL, "bad punctured / shortened lists");
+    std::vector<uint8_t> cls(g->n, 0);
+    std::vector<int32_t> src(g->n, 0);
+    for (int i = 0; i < n_punct; ++i) {
+        if (punctured[i] < 0 || punctured[i] >= g->n || (i && punctured[i] <= punctured[i - 1]))
+            return fail(QLDPC_EINVAL, "punctured positions must be ascending and in [0, n)");
+        cls[punctured[i]] = 1;
+        src[punctured[i]] = i;
+    }
+    for (int i = 0; i < n_short; ++i) {
+        if (shortened[i] < 0 || shortened[i] >= g->n || (i && shortened[i] <= shortened[i - 1]))
+            return fail(QLDPC_EINVAL, "shortened positions must be ascending and in [0, n)");
+        if (cls[shortened[i]]) return fail(QLDPC_EINVAL, "a position is both punctured and shortened");
+        cls[shortened[i]] = 2;
+    }
+    int key = 0;
+    for (int i = 0; i < g->n; ++i)
+        if (cls[i] == 0) src[i] = key++;
+    auto plan = std::make_unique<qldpc_rate_plan>();
+    plan->n_punct = n_punct;
+    plan->n_short = n_short;
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    for (auto &dg : g->devs) {
+        HIP_TRY(hipSetDevice(dg->device));
+        uint8_t *dc = nullptr;
+        int32_t *ds = nullptr;
+        int rc;
+        if ((rc = upload(&dc, cls)) || (rc = upload(&ds, src))) {
+            (void)hipSetDevice(prev);
+            return rc;
+        }
+        plan->devs.push_back({dg->device, dc, ds});
+    }
+    HIP_TRY(hipSetDevice(prev));
+    *out = plan.release();
+    return QLDPC_OK;
+}
+
+void qldpc_rate_plan_destroy(qldpc_rate_plan *plan) {
+    if (!plan) return;
+    for (auto &d : plan->devs) {
+        (void)hipFree(d.cls);
+        (void)hipFree(d.src);
+    }
+    delete plan;
+}
+
+int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
+                                   int32_t n_punct, uint8_t *d_alice, uint8_t *d_bob, uint8_t *d_punct_alice,
+                                   uint8_t *d_punct_bob, double *accurate_qber_out, void *stream) {
+    if (n_punct < 0 || (n_punct > 0 && batch > 0 && (!d_punct_alice || !d_punct_bob)))
+        return fail(QLDPC_EINVAL, "bad n_punct / NULL punctured-draw buffers");
+    if (n <= 0 || batch < 0) return fail(QLDPC_EINVAL, "n must be > 0 and batch >= 0");
+    const uint64_t n_err = (uint64_t)((double)n * qber);
+    if (n_err == 0) return fail(QLDPC_EINVAL, "Key size '" + std::to_string(n) + "' is too small for QBER.");
+    if (n_err > (uint64_t)n) return fail(QLDPC_EINVAL, "QBER must be <= 1");
+    if (accurate_qber_out) *accurate_qber_out = (double)n_err / (double)n;
+    if (batch == 0) return QLDPC_OK;
+    if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
+    const hipStream_t s = (hipStream_t)stream;
+    uint32_t *scratch = nullptr;
+    const size_t words = trials_scratch_words(n, batch);
+    if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
+    hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, n_punct, d_punct_alice,
+                                 d_punct_bob, s);
+    if (scratch) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(scratch);
+    }
+    if (e != hipSuccess) return hip_fail(e, "trials_rate_adapt");
+    return QLDPC_OK;
+}
+
+int qldpc_build_frames_rate_adapt_device(qldpc_graph *g, const qldpc_rate_plan *plan, int32_t device, int32_t batch,
+                                         const uint8_t *d_alice, const uint8_t *d_bob, const uint8_t *d_punct_alice,
+                                         const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext,
+                                         double *d_llr, uint8_t *d_syndrome, void *stream) {
+    if (!g || !plan) return fail(QLDPC_EINVAL, "graph / plan is NULL");
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch > 0 && (!d_alice || !d_bob || !d_log_p || !d_alice_ext || !d_llr || !d_syndrome ||
+                      (plan->n_punct && (!d_punct_alice || !d_punct_bob))))
+        return fail(QLDPC_EINVAL, "NULL device buffer");
+    DeviceGraph *dg = find_dev(g, device);
+    const qldpc_rate_plan::Dev *pd = nullptr;
+    for (auto &d : plan->devs)
+        if (d.device == device) pd = &d;
+    if (!dg || !pd) return fail(QLDPC_EINVAL, "graph / plan does not live on that device");
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    hipError_t e = launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
+                                          d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, d_llr,
+                                          d_syndrome, nullptr, nullptr, nullptr, (hipStream_t)stream);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return hip_fail(e, "build_frames_rate_adapt");
+    return QLDPC_OK;
+}
+
+int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan *plan, int32_t device,
+                                           const qldpc_params *p, int32_t batch, const uint8_t *d_alice,
+                                           const uint8_t *d_bob, const uint8_t *d_punct_alice,
+                                           const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext,
+                                           double *d_llr_ws, uint8_t *d_synd_ws, uint8_t *d_bits_out,
+                                           uint32_t *d_iters_out, uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out,
+                                           void *stream) {
+    if (!g || !plan) return fail(QLDPC_EINVAL, "graph / plan is NULL");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
+    if (batch == 0) return QLDPC_OK;
+    if (!d_alice || !d_bob || !d_log_p || !d_alice_ext || !d_llr_ws || !d_synd_ws || !d_bits_out || !d_iters_out ||
+        !d_synd_ok_out || (plan->n_punct && (!d_punct_alice || !d_punct_bob)))
+        return fail(QLDPC_EINVAL, "NULL device buffer");
+    DeviceGraph *dg = find_dev(g, device);
+    const qldpc_rate_plan::Dev *pd = nullptr;
+    for (auto &d : plan->devs)
+        if (d.device == device) pd = &d;
+    if (!dg || !pd) return fail(QLDPC_EINVAL, "graph / plan does not live on that device");
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    const hipStream_t s = (hipStream_t)stream;
+    auto body = [&]() -> int {
+        uint8_t *codes = nullptr, *pal_ok = nullptr;
+        double *palette = nullptr;
+        if (g->variant == VAR_V2) {
+            std::lock_guard<std::mutex> lk(dg->mu);
+            Workspace *w = workspace(dg, s);
+            int r = ensure_codes(g, w, batch, s);
+            if (r) return r;
+            codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
+        }
+        HIP_TRY(launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
+                                       d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, d_llr_ws,
+                                       d_synd_ws, codes, palette, pal_ok, s));
+        int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
+                          g->variant == VAR_V2);
+        if (r) return r;
+        // keys_match = arrays_equal(alice_extended, bob_solution) (:1216)
+        if (d_keys_match_out) HIP_TRY(launch_keys_match(batch, g->n, d_alice_ext, d_bits_out, d_keys_match_out, s));
+        return QLDPC_OK;
+    };
+    rc = body();
+    (void)hipSetDevice(prev);
+    return rc;
+}
+
 // ---- trial generator (src/simulation.cpp:540-551,713-719,743) ----------------
 int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_out) {
     if (count < 0 || (count > 0 && !seeds_out)) return fail(QLDPC_EINVAL, "bad count / NULL seeds_out");
-    // Xoshiro256++ seeded by four SplitMix64 outputs (Xoshiro-cpp); the
-    // reference draws seeds with uniform_int_distribution<size_t>(0, SIZE_MAX),
-    // which passes each 64-bit output through unchanged.
-    uint64_t st[4], x = simulation_seed;
-    for (auto &v : st) {
-        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
-        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-        v = z ^ (z >> 31);
-    }
-    auto rotl = [](uint64_t v, int k) { return (v << k) | (v >> (64 - k)); };
-    for (int32_t i = 0; i < count; ++i) {
-        seeds_out[i] = rotl(st[0] + st[3], 23) + st[0];
-        const uint64_t t = st[1] << 17;
-        st[2] ^= st[0];
-        st[3] ^= st[1];
-        st[1] ^= st[2];
-        st[0] ^= st[3];
-        st[2] ^= t;
-        st[3] = rotl(st[3], 45);
-    }
+    // The reference draws seeds with uniform_int_distribution<size_t>(0,
+    // SIZE_MAX), which passes each 64-bit output through unchanged.
+    Xoshiro256pp g(simulation_seed);
+    std::uniform_int_distribution<size_t> d(0, std::numeric_limits<size_t>::max());
+    for (int32_t i = 0; i < count; ++i) seeds_out[i] = d(g);
     return QLDPC_OK;
 }
 
@@ -924,7 +1161,7 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
     uint32_t *scratch = nullptr;
     const size_t words = trials_scratch_words(n, batch);
     if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
-    hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, s);
+    hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, 0, nullptr, nullptr, s);
     if (scratch) {
         (void)hipStreamSynchronize(s);
         (void)hipFree(scratch);

@@ -115,7 +115,13 @@ hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t
 size_t trials_lds_bytes(int n);
 size_t trials_scratch_words(int n, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
-                         uint8_t *bob, uint32_t *scratch, hipStream_t stream);
+                         uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
+                         hipStream_t stream);
+hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const int32_t *row_deg, const uint8_t *cls,
+                                  const int32_t *src, int n_punct, int batch, const uint8_t *alice, const uint8_t *bob,
+                                  const uint8_t *palice, const uint8_t *pbob, const double *log_p, uint8_t *alice_ext,
+                                  double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
+                                  hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
                              uint8_t *match, hipStream_t stream);

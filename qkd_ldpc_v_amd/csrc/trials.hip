@@ -68,7 +68,8 @@ __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
 template <typename IDX, bool IN_LDS>
 __global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
                                                     uint64_t seed_add, uint8_t *alice, uint8_t *bob,
-                                                    uint32_t *scratch) {
+                                                    uint32_t *scratch, int n_punct, uint8_t *punct_alice,
+                                                    uint8_t *punct_bob) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int f = blockIdx.x;
     if (f >= batch) return;
@@ -130,6 +131,14 @@ __global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int b
                 flips[p >> 5] |= 1u << (p & 31);
             }
         }
+        // QKD_LDPC_RATE_ADAPT continues the trial's generator: two
+        // uniform_int_distribution<int>(0, 1) draws (Alice, then Bob) per
+        // punctured position, in ascending position order
+        // (src/qkd_ldpc_algorithm.cpp:1148-1157).
+        for (int j = 0; j < n_punct; ++j) {
+            punct_alice[(size_t)f * n_punct + j] = (uint8_t)(g.next() >> 63);
+            punct_bob[(size_t)f * n_punct + j] = (uint8_t)(g.next() >> 63);
+        }
     }
     __syncthreads();
     uint8_t *a = alice + (size_t)f * n;
@@ -142,7 +151,78 @@ __global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int b
     }
 }
 
+// QKD_LDPC_RATE_ADAPT's extended frame (src/qkd_ldpc_algorithm.cpp:1121-1180):
+// position i is a key bit (cls 0: the next trial key bit, LLR +-log_p), a
+// punctured bit (cls 1: the trial's extra draws, LLR ALMOST_ZERO = 1e-4) or a
+// shortened bit (cls 2: 0 on both sides, LLR DBL_MAX); src[i] indexes the key
+// or punctured draw.  Writes Alice's extended key, optionally the LLRs, the
+// V2 palette form (codes 0/1 = +-log_p, 2 = 1e-4, 3 = DBL_MAX) and the Alice
+// syndrome of the extended key.
+__global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, const int32_t *ell_col,
+                                                              const int32_t *row_deg, const uint8_t *cls,
+                                                              const int32_t *src, int n_punct,
+                                                              const uint8_t *alice, const uint8_t *bob,
+                                                              const uint8_t *palice, const uint8_t *pbob,
+                                                              const double *log_p, uint8_t *alice_ext, double *llr,
+                                                              uint8_t *synd, uint8_t *codes, double *palette,
+                                                              uint8_t *pal_ok) {
+    const size_t f = blockIdx.x;
+    const double lp = log_p[f];
+    const uint8_t *al = alice + f * (size_t)n;
+    const uint8_t *bo = bob + f * (size_t)n;
+    const uint8_t *pa = palice + f * (size_t)n_punct;
+    (void)pbob;  // Bob's punctured draws only advance the generator (LLR = ALMOST_ZERO)
+    uint8_t *ax = alice_ext + f * (size_t)n;
+    auto bob_code = [&](int i) -> int {  // palette code of position i
+        const int c = cls[i];
+        if (c == 0) return bo[src[i]] ? 1 : 0;
+        return c == 1 ? 2 : 3;
+    };
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int c = cls[i];
+        ax[i] = c == 0 ? al[src[i]] : (c == 1 ? pa[src[i]] : 0);
+        if (llr) {
+            const int code = bob_code(i);
+            llr[f * (size_t)n + i] = code == 0 ? lp : code == 1 ? -lp : code == 2 ? 1e-4 : 1.7976931348623157e308;
+        }
+    }
+    if (codes) {
+        const int nc = (n + 3) / 4;
+        uint8_t *cs = codes + f * (size_t)nc;
+        for (int j = threadIdx.x; j < nc; j += blockDim.x) {
+            int byte = 0;
+            for (int q = 0; q < 4; ++q)
+                if (4 * j + q < n) byte |= bob_code(4 * j + q) << (2 * q);
+            cs[j] = (uint8_t)byte;
+        }
+        if (threadIdx.x < 4) {
+            const double pv[4] = {lp, -lp, 1e-4, 1.7976931348623157e308};
+            palette[f * 4 + threadIdx.x] = pv[threadIdx.x];
+        }
+        if (threadIdx.x == 0) pal_ok[f] = 1;
+    }
+    __syncthreads();  // the extended key is complete (global, this block)
+    uint8_t *s = synd + f * (size_t)m;
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        int p = 0;
+        const int deg = row_deg[j];
+        for (int k = 0; k < deg; ++k) p ^= ax[ell_col[(size_t)k * m + j]];
+        s[j] = (uint8_t)(p & 1);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const int32_t *row_deg, const uint8_t *cls,
+                                  const int32_t *src, int n_punct, int batch, const uint8_t *alice, const uint8_t *bob,
+                                  const uint8_t *palice, const uint8_t *pbob, const double *log_p, uint8_t *alice_ext,
+                                  double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
+                                  hipStream_t stream) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, cls, src,
+                       n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok);
+    return hipGetLastError();
+}
 
 size_t trials_lds_bytes(int n) {
     const size_t words = (size_t)(n + 31) / 32;
@@ -152,7 +232,8 @@ size_t trials_lds_bytes(int n) {
 size_t trials_scratch_words(int n, int batch) { return n <= 65536 ? 0 : (size_t)n * (size_t)batch; }
 
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
-                         uint8_t *bob, uint32_t *scratch, hipStream_t stream) {
+                         uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
+                         hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     const size_t lds = trials_lds_bytes(n);
     if (n <= 65536) {
@@ -161,14 +242,14 @@ hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
-                           scratch);
+                           scratch, n_punct, punct_alice, punct_bob);
     } else {
         auto k = trials_kernel<uint32_t, false>;
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
-                           scratch);
+                           scratch, n_punct, punct_alice, punct_bob);
     }
     return hipGetLastError();
 }

@@ -178,6 +178,49 @@ class Graph:
             keys_match.data_ptr(), _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_batch_device")
 
 
+    def rate_plan(self, punctured, shortened) -> "RatePlan":
+        return RatePlan(self, punctured, shortened)
+
+    def qkd_ldpc_rate_adapt_device(self, plan: "RatePlan", params: Params, alice, bob, punct_alice, punct_bob, log_p,
+                                   alice_ext, llr_ws, synd_ws, bits, iters, ok, keys_match, stream=None,
+                                   device: int | None = None) -> None:
+        """QKD_LDPC_RATE_ADAPT's per-trial window for a batch, all on device."""
+        dev = alice.device.index if device is None else device
+        p = params.c()
+        check(lib().qldpc_qkd_ldpc_rate_adapt_batch_device(
+            self._g, plan.handle, dev, ctypes.byref(p), int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(),
+            punct_alice.data_ptr(), punct_bob.data_ptr(), log_p.data_ptr(), alice_ext.data_ptr(), llr_ws.data_ptr(),
+            synd_ws.data_ptr(), bits.data_ptr(), iters.data_ptr(), ok.data_ptr(), keys_match.data_ptr(),
+            _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_rate_adapt_batch_device")
+
+    def build_frames_rate_adapt_device(self, plan: "RatePlan", alice, bob, punct_alice, punct_bob, log_p, alice_ext,
+                                       llr, syndrome, stream=None, device: int | None = None) -> None:
+        dev = alice.device.index if device is None else device
+        check(lib().qldpc_build_frames_rate_adapt_device(
+            self._g, plan.handle, dev, int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(), punct_alice.data_ptr(),
+            punct_bob.data_ptr(), log_p.data_ptr(), alice_ext.data_ptr(), llr.data_ptr(), syndrome.data_ptr(),
+            _stream_ptr(stream, dev)), "qldpc_build_frames_rate_adapt_device")
+
+
+class RatePlan:
+    """Punctured / shortened positions of one adapted rate, on the graph's devices."""
+
+    def __init__(self, graph: Graph, punctured, shortened):
+        self.punctured = np.ascontiguousarray(punctured, np.int32)
+        self.shortened = np.ascontiguousarray(shortened, np.int32)
+        h = ctypes.c_void_p()
+        check(lib().qldpc_rate_plan_create(graph.handle, self.punctured.size, self.punctured.ctypes.data,
+                                           self.shortened.size, self.shortened.ctypes.data, ctypes.byref(h)),
+              "qldpc_rate_plan_create")
+        self.handle = h
+        self._graph = graph  # keep the graph alive
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            lib().qldpc_rate_plan_destroy(self.handle)
+            self.handle = None
+
+
 def keys_match_device(alice, bits, out, stream=None) -> None:
     dev = alice.device.index
     check(lib().qldpc_keys_match_device(int(alice.shape[0]), int(alice.shape[1]), alice.data_ptr(), bits.data_ptr(),
@@ -203,6 +246,48 @@ def trials_device(n: int, qber: float, seeds, alice, bob, seed_add: int = 0, str
     check(lib().qldpc_trials_device(int(n), float(qber), int(seeds.shape[0]), seeds.data_ptr(),
                                     int(seed_add) & 0xFFFFFFFFFFFFFFFF, alice.data_ptr(), bob.data_ptr(),
                                     ctypes.byref(q), _stream_ptr(stream, dev)), "qldpc_trials_device")
+    return q.value
+
+
+def xoshiro_state(seed: int) -> np.ndarray:
+    st = np.empty(4, np.uint64)
+    check(lib().qldpc_xoshiro_state(int(seed) & 0xFFFFFFFFFFFFFFFF, st.ctypes.data), "qldpc_xoshiro_state")
+    return st
+
+
+def adapt_code_rate(n: int, m: int, qber: float, delta: float, efficiency: float, untainted=None, state=None):
+    """adapt_code_rate (src/array_and_matrix_operations.cpp:1131-1223).
+    state: np.uint64[4] generator state, advanced in place (chain calls like the
+    reference's setup loop).  -> (punctured, shortened, adapted_rate); empty
+    lists for the reference's skipped (out-of-range) combinations."""
+    import ctypes
+
+    if state is None:
+        raise ValueError("pass the generator state (xoshiro_state(seed))")
+    unt = None if untainted is None else np.ascontiguousarray(untainted, np.int32)
+    p = np.empty(n, np.int32)
+    s = np.empty(n, np.int32)
+    npn, nsn = ctypes.c_int32(0), ctypes.c_int32(0)
+    rate = ctypes.c_double(0.0)
+    check(lib().qldpc_adapt_code_rate(n, m, qber, delta, efficiency, 0 if unt is None else 1,
+                                      None if unt is None else unt.ctypes.data, 0 if unt is None else unt.size,
+                                      state.ctypes.data, p.ctypes.data, ctypes.byref(npn), s.ctypes.data,
+                                      ctypes.byref(nsn), ctypes.byref(rate)), "qldpc_adapt_code_rate")
+    return p[:npn.value].copy(), s[:nsn.value].copy(), rate.value
+
+
+def trials_rate_adapt_device(n: int, qber: float, seeds, n_punct: int, alice, bob, punct_alice, punct_bob,
+                             seed_add: int = 0, stream=None) -> float:
+    """trials_device plus QKD_LDPC_RATE_ADAPT's punctured draws (2 per position)."""
+    import ctypes
+
+    dev = seeds.device.index
+    q = ctypes.c_double(0.0)
+    check(lib().qldpc_trials_rate_adapt_device(int(n), float(qber), int(seeds.shape[0]), seeds.data_ptr(),
+                                               int(seed_add) & 0xFFFFFFFFFFFFFFFF, int(n_punct), alice.data_ptr(),
+                                               bob.data_ptr(), punct_alice.data_ptr(), punct_bob.data_ptr(),
+                                               ctypes.byref(q), _stream_ptr(stream, dev)),
+          "qldpc_trials_rate_adapt_device")
     return q.value
 
 
