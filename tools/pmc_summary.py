@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch means of rocprofv3 PMC counters for kernels matching a pattern.
 
-usage: tools/pmc_summary.py <prof_dir> [kernel_substring] [--json out.json]
+usage: tools/pmc_summary.py <prof_dir> [kernel_substring] [--prefix P] [--json out.json]
 Sums each counter over its per-XCD/SE rows per dispatch, then averages over
 dispatches of the matching kernel (warm-up launch included)."""
 import collections
@@ -12,9 +12,9 @@ import os
 import sys
 
 
-def summarize(prof_dir, pat="decode"):
+def summarize(prof_dir, pat="decode", prefix=""):
     out = {}
-    for f in sorted(glob.glob(os.path.join(prof_dir, "*", "run_counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(prof_dir, prefix + "*", "run_counter_collection.csv"))):
         byd = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in csv.DictReader(open(f)):
             if pat in r["Kernel_Name"]:
@@ -25,9 +25,21 @@ def summarize(prof_dir, pat="decode"):
 
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    res = summarize(args[0], args[1] if len(args) > 1 else "decode")
+    argv = sys.argv[1:]
+    prefix = ""
+    if "--prefix" in argv:
+        i = argv.index("--prefix")
+        prefix = argv[i + 1]
+        del argv[i:i + 2]
+    if "--json" in argv:
+        i = argv.index("--json")
+        jpath = argv[i + 1]
+        del argv[i:i + 2]
+    else:
+        jpath = None
+    args = argv
+    res = summarize(args[0], args[1] if len(args) > 1 else "decode", prefix)
     for k in sorted(res):
         print(f"{k:32s} {res[k]:.6g}")
-    if "--json" in sys.argv:
-        json.dump(res, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+    if jpath:
+        json.dump(res, open(jpath, "w"), indent=1)
