@@ -78,6 +78,7 @@ struct DeviceGraph {
     uint64_t *vn_mask = nullptr, *vn_mask_ms = nullptr; // V2: [wave][dv_max] slot masks
     uint32_t *slot_meta2 = nullptr, *slot_meta2_ms = nullptr;  // V2 hybrid: stage index per slot
     int32_t *hd_bits = nullptr, *hd_dv = nullptr, *stage_off = nullptr;
+    int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
     int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
@@ -135,7 +136,9 @@ struct Xoshiro256pp {
 struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
     int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
-    std::vector<int> wave_rows;             // V2: first row of each wave (+ m)
+    std::vector<int> wave_rows;             // V2: first layout row of each wave (+ m)
+    std::vector<int> row_order;             // V2: layout row -> original row
+    std::vector<int> layout_row_ptr;        // V2: row_ptr of the rows in layout order
     int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     std::vector<std::unique_ptr<DeviceGraph>> devs;
@@ -193,6 +196,81 @@ void plan(qldpc_graph &g) {
 // and barrier cost), capped by the instantiation's workgroup size; R is the
 // smallest register-slot instantiation that holds the plan.  QLDPC_V2_WAVES
 // forces W.  Returns false when no V2 instantiation fits (v1 is used).
+// Deal rows to W waves so that every wave's edge count is at most cap when
+// possible: contiguous blocks of rows first (consecutive check ids keep the
+// VN phase masks sparse), then swap / move single rows between the heaviest
+// and lightest waves.  Returns wave membership lists and the sums.
+std::vector<std::vector<int>> balance_rows(const int32_t *row_ptr, int m, int W, long long cap,
+                                           std::vector<long long> &sums) {
+    auto deg = [&](int j) { return row_ptr[j + 1] - row_ptr[j]; };
+    const long long E = row_ptr[m];
+    std::vector<std::vector<int>> waves(W);
+    sums.assign(W, 0);
+    {
+        int j = 0;
+        for (int w = 0; w < W; ++w) {
+            const long long target = E * (w + 1) / W;
+            while (j < m && (w == W - 1 || row_ptr[j + 1] <= target ||
+                             (row_ptr[j] < target && target - row_ptr[j] > row_ptr[j + 1] - target))) {
+                waves[w].push_back(j);
+                sums[w] += deg(j);
+                ++j;
+            }
+        }
+    }
+    // degree -> rows, per wave
+    std::vector<std::map<int, std::vector<int>>> by(W);
+    for (int w = 0; w < W; ++w)
+        for (int j : waves[w]) by[w][deg(j)].push_back(j);
+    for (int iter = 0; iter < 100000; ++iter) {
+        const int H = (int)(std::max_element(sums.begin(), sums.end()) - sums.begin());
+        const int L = (int)(std::min_element(sums.begin(), sums.end()) - sums.begin());
+        if (sums[H] <= cap || H == L) break;
+        const long long gap = sums[H] - sums[L];
+        // best transfer d (row of degree dx from H, optionally one of degree dy from L)
+        long long best = 0;
+        int bx = -1, by_ = -1;
+        for (auto &kx : by[H]) {
+            if (kx.second.empty()) continue;
+            const long long dx = kx.first;
+            if (dx < gap && dx > best) best = dx, bx = kx.first, by_ = -1;  // move
+            for (auto &ky : by[L]) {
+                if (ky.second.empty()) continue;
+                const long long d = dx - ky.first;
+                if (d > 0 && d < gap && d > best) best = d, bx = kx.first, by_ = ky.first;
+            }
+        }
+        if (best == 0) break;
+        // never overshoot: the new max of the pair must drop
+        const int x = by[H][bx].back();
+        by[H][bx].pop_back();
+        by[L][bx].push_back(x);
+        sums[H] -= bx;
+        sums[L] += bx;
+        if (by_ >= 0) {
+            const int y = by[L][by_].back();
+            by[L][by_].pop_back();
+            by[H][by_].push_back(y);
+            sums[L] -= by_;
+            sums[H] += by_;
+        }
+    }
+    for (int w = 0; w < W; ++w) {
+        waves[w].clear();
+        for (auto &kv : by[w]) waves[w].insert(waves[w].end(), kv.second.begin(), kv.second.end());
+        std::sort(waves[w].begin(), waves[w].end());
+    }
+    return waves;
+}
+
+// V2 plan: rows dealt to W waves (balanced by edge count, rows relabelled so
+// each wave holds a contiguous block of layout rows), each wave's edges dealt
+// EPL_w per lane to its 64 lanes (EPL_w >= max_dc keeps a row within two
+// adjacent lanes of ONE wave).  W is the fewest waves whose lanes do not need
+// more than max_dc slots (more would only add idle waves and barrier cost),
+// capped by the instantiation's workgroup size; the shape is the smallest
+// slot count that holds the plan.  QLDPC_V2_WAVES forces W.  Returns false when
+// no V2 instantiation fits (v1 is used).
 bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
     // head <= 31 (tail parity in a 32-bit mask), dummy column id n < 2^20
     if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
@@ -208,29 +286,29 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         W = std::max(1, W);
         if (W > wmax) continue;
         if (lds_bytes_v2(2, g.n, g.m, W * 64) > LDS_LIMIT) continue;
-        std::vector<int> rb(W + 1, g.m);
-        rb[0] = 0;
-        for (int w = 1; w < W; ++w) {
-            const long long target = E * w / W;
-            int j = rb[w - 1];
-            while (j < g.m && row_ptr[j + 1] <= target) ++j;  // rows ending at or before target
-            if (j < g.m && target - row_ptr[j] > row_ptr[j + 1] - target) ++j;  // nearer boundary
-            rb[w] = j;
+        const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
+        std::vector<long long> sums;
+        const auto waves = balance_rows(row_ptr, g.m, W, cap, sums);
+        std::vector<int> order, rb(W + 1, 0), nrp(g.m + 1, 0);
+        for (int w = 0; w < W; ++w) {
+            order.insert(order.end(), waves[w].begin(), waves[w].end());
+            rb[w + 1] = (int)order.size();
         }
+        for (int j = 0; j < g.m; ++j) nrp[j + 1] = nrp[j] + (row_ptr[order[j] + 1] - row_ptr[order[j]]);
         int epl = 0;
         bool ok = true;
         for (int w = 0; w < W && ok; ++w) {
-            const long long ew = row_ptr[rb[w + 1]] - row_ptr[rb[w]];
+            const long long ew = nrp[rb[w + 1]] - nrp[rb[w]];
             if (ew == 0) continue;
             const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
             ok = e <= R;
             epl = std::max(epl, e);
             // rows started per lane must fit the 32-bit syndrome mask
             for (long long l = 0; l < 64 && ok; ++l) {
-                const long long e0 = row_ptr[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, row_ptr[rb[w + 1]]);
+                const long long e0 = nrp[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, nrp[rb[w + 1]]);
                 int starts = 0;
                 for (int j = rb[w]; j < rb[w + 1]; ++j)
-                    if (row_ptr[j] >= e0 && row_ptr[j] < e1) ++starts;
+                    if (nrp[j] >= e0 && nrp[j] < e1) ++starts;
                 ok = starts <= 32;
             }
         }
@@ -241,6 +319,8 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         g.T = W * 64;
         g.EPL = epl;
         g.wave_rows = rb;
+        g.row_order = order;
+        g.layout_row_ptr = nrp;
         return true;
     }
     return false;
@@ -323,8 +403,21 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // aggregate and parity are order-free, and grouping a
     // row's k-th bit edges lets the VN phase masks skip more slots.  SPA keeps
     // CSR order (its row product is sequential, :57-62).
-    std::vector<int> perm(E);
-    for (int e = 0; e < E; ++e) perm[e] = e;
+    // Layout order: V2 relabels rows (plan_v2 balances waves); lrp / lrow /
+    // ledge give, per position of the layout's row-major edge list, its row
+    // and its original CSR edge.  v1 keeps the original order.
+    std::vector<int> lrp(row_ptr, row_ptr + m + 1), lrow(row_of), ledge(E), perm(E);
+    for (int e = 0; e < E; ++e) ledge[e] = e;
+    if (v2) {
+        lrp = g->layout_row_ptr;
+        for (int j = 0; j < m; ++j) {
+            const int r = g->row_order[j];
+            for (int t = 0; t < row_ptr[r + 1] - row_ptr[r]; ++t) {
+                lrow[lrp[j] + t] = j;
+                ledge[lrp[j] + t] = row_ptr[r] + t;
+            }
+        }
+    }
     // Hybrid shape: VN terms kk >= vn_k0 go through a per-frame stage, laid out
     // term-major over the bits of degree > kk, bits ordered by degree
     // (descending) so each term's bits are a prefix: stage[off[kk] + rank[b]].
@@ -352,13 +445,14 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         mt.assign((size_t)G4 * TS * 4, 0);
         mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
+        perm = ledge;
         if (sorted)
             for (int j = 0; j < m; ++j)
-                std::stable_sort(perm.begin() + row_ptr[j], perm.begin() + row_ptr[j + 1],
+                std::stable_sort(perm.begin() + lrp[j], perm.begin() + lrp[j + 1],
                                  [&](int x, int y) { return kpos[x] < kpos[y]; });
         for (int w = 0; w < W; ++w) {
-            const long long wb = v2 ? row_ptr[g->wave_rows[w]] : 0;
-            const long long we = v2 ? row_ptr[g->wave_rows[w + 1]] : E;
+            const long long wb = v2 ? lrp[g->wave_rows[w]] : 0;
+            const long long we = v2 ? lrp[g->wave_rows[w + 1]] : E;
             const int lanes = v2 ? 64 : T;
             const int epl_w = v2 ? std::max<int>((int)((we - wb + 63) / 64), g->max_dc) : EPL;
             for (int li = 0; li < lanes; ++li) {
@@ -368,9 +462,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                 int head = 0;
                 lnst[l] = 0;
                 if (e0 < we) {
-                    const int r0 = row_of[e0];
+                    const int r0 = lrow[e0];
                     lrow0[l] = r0;
-                    if (e0 != row_ptr[r0]) head = lhead[l] = row_ptr[r0 + 1] - (int)e0;
+                    if (e0 != lrp[r0]) head = lhead[l] = lrp[r0 + 1] - (int)e0;
                 }
                 int prev_row = -1;
                 for (int k = 0; k < (v2 ? G4 * 4 : epl_w); ++k) {
@@ -380,18 +474,18 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         if (!v2) break;
                         wd = DUMMY;
                     } else {
-                        const int j = row_of[e];
+                        const int j = lrow[e];
                         const int ed = perm[e];  // the edge at that position
                         wd = (uint32_t)col_idx[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
                         if (v2) vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
                             mt2[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] =
                                 (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
-                        if (e == row_ptr[j]) {
+                        if (e == lrp[j]) {
                             wd |= META_START;
                             ++lnst[l];
                         }
-                        if (e == row_ptr[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
+                        if (e == lrp[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
                         if (k > 0 && j != prev_row && j != prev_row + 1)
                             return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
                         prev_row = j;
@@ -402,6 +496,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
         return QLDPC_OK;
     };
+    std::vector<int32_t> row_orig(v2 ? g->row_order : std::vector<int>());
     std::vector<uint32_t> meta_ms, meta2, meta2_ms;
     std::vector<uint64_t> vnm, vnm_ms;
     int brc = build_meta(false, meta, vnm, meta2);
@@ -455,7 +550,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->vn_mask, vnm)) || (rc = upload(&dg->vn_mask_ms, vnm_ms)) ||
             (rc = upload(&dg->slot_meta2, meta2)) || (rc = upload(&dg->slot_meta2_ms, meta2_ms)) ||
             (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
-            (rc = upload(&dg->stage_off, stage_off)) ||
+            (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
             (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
@@ -569,6 +664,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.vn_k0 = g->vn_k0; a.n_hd = g->n_hd; a.hd_bits = dg->hd_bits; a.hd_dv = dg->hd_dv; a.stage_off = dg->stage_off;
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
+    a.row_orig = dg->row_orig;
     a.nc = (g->n + 3) / 4;
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
     a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
@@ -703,6 +799,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->hd_bits);
         (void)hipFree(d->hd_dv);
         (void)hipFree(d->stage_off);
+        (void)hipFree(d->row_orig);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->lane_epl);

@@ -90,6 +90,7 @@ struct DecodeArgs {
     const int32_t *stage_off;       // [dv_max]: offset of term kk's block in the stage
     const uint32_t *slot_meta2;     // like slot_meta: stage index of the slot's edge
     long long stage_wg_offset;      // doubles from a workgroup's scratch base to its stage
+    const int32_t *row_orig;        // V2: layout row -> original row (syndrome index)
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.

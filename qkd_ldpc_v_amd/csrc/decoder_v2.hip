@@ -114,12 +114,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const uint8_t *sy = a.synd + (size_t)f * m;
         // Target syndrome bits of the rows this lane starts (bit i = i-th START),
         // and of the row it finishes for the lane before (split row).
+        // (rows are relabelled by the planner: row_orig maps them back)
         uint32_t smask_f = 0;
         {
             const int rs = row0_in + (head_in > 0 ? 1 : 0);
-            for (int i = 0; i < nst; ++i) smask_f |= (uint32_t)(sy[rs + i] & 1) << i;
+            for (int i = 0; i < nst; ++i) smask_f |= (uint32_t)(sy[a.row_orig[rs + i]] & 1) << i;
         }
-        const int s_row0 = (head_in > 0) ? (sy[row0_in] & 1) : 0;
+        const int s_row0 = (head_in > 0) ? (sy[a.row_orig[row0_in]] & 1) : 0;
         const bool paletted = a.pal_ok[f] != 0;
         // Non-paletted frames gather llr[] through a buffer resource: a distinct
         // load kind the compiler cannot fuse with the LDS palette read into a
