@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded info-bits/sec (whole node), n=10k R=0.8 SPA 50-iter, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_WAVE_INSTR = 5.09e11  # measured: tools/valu_bench.hip, independent v_fma_f64 chains, 256 CUs
 
 WORKLOADS = {
     # name: matrix fixture, format, algorithm, primary, secondary, qber, batch/GPU, description
@@ -205,10 +206,13 @@ def main():
         # per-launch algorithmic bytes of THIS rank's decode kernel / its mean duration
         achieved = (it_sum * B) / (kernel_ms * 1e-3) / 1e9
         traffic = None
+        valu_per_launch = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pm = json.load(f)
+            traffic = pm.get("hbm_bytes_per_launch")
+            valu_per_launch = pm.get("valu_wave_instructions_per_launch")
         res = {
             "metric": METRIC,
             "value": value,
@@ -250,6 +254,15 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if valu_per_launch:
+            # The decode kernel keeps messages on chip: it is bound by FP64 VALU
+            # issue, not HBM.  VALU wave-instructions per launch from the PMC
+            # pass (profiles/pmc_<workload>.json) over this run's kernel time,
+            # against the whole-chip VALU issue rate tools/valu_bench.hip
+            # measures (profiles/r01/valu_microbench.json).
+            ach = valu_per_launch / (kernel_ms * 1e-3)
+            res["compute_roofline"] = {"bound": "fp64-valu-issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR,
+                                       "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WAVE_INSTR}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
                                                args.cpu_baseline_seconds, k_info,

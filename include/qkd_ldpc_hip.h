@@ -230,6 +230,20 @@ int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan
                                            uint32_t *d_iters_out, uint8_t *d_synd_ok_out, uint8_t *d_keys_match_out,
                                            void *stream);
 
+/* ---- Simulation-driver helpers ----------------------
+ * qldpc_sort_permutation: the order std::sort (libstdc++, not stable) leaves a
+ * sequence in when comparing only `keys` — how the reference orders its
+ * config maps by code_rate (src/config.cpp:43,289,355,389).
+ * qldpc_bits_to_remove: privacy-maintenance bit positions
+ * (get_bits_positions_to_remove / _rate_adapt,
+ * src/array_and_matrix_operations.cpp:138-256), ascending; out needs capacity
+ * n (NULL: count only).  The out-key length of the throughput columns is
+ * n - count. */
+int qldpc_sort_permutation(const double *keys, int32_t n, int32_t *perm_out);
+int qldpc_bits_to_remove(int32_t n, int32_t m, const int32_t *col_ptr, const int32_t *row_idx, int32_t n_punct,
+                         const int32_t *punctured, int32_t n_short, const int32_t *shortened, int32_t rate_adapt,
+                         int32_t *out, int32_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,6 +70,8 @@ _SIGNATURES = {
     "qldpc_selftest_math_device": (_I32, [_I32, _I32, _P, _P, _P]),
     "qldpc_trial_seeds": (_I32, [ctypes.c_uint64, _I32, _P]),
     "qldpc_xoshiro_state": (_I32, [ctypes.c_uint64, _P]),
+    "qldpc_sort_permutation": (_I32, [_P, _I32, _P]),
+    "qldpc_bits_to_remove": (_I32, [_I32, _I32, _P, _P, _I32, _P, _I32, _P, _I32, _P, _PI32]),
     "qldpc_adapt_code_rate": (_I32, [_I32, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double, _I32, _P, _I32,
                                      _P, _P, _PI32, _P, _PI32, ctypes.POINTER(ctypes.c_double)]),
     "qldpc_rate_plan_create": (_I32, [_P, _I32, _P, _I32, _P, ctypes.POINTER(_P)]),

@@ -1233,6 +1233,67 @@ int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan
     return rc;
 }
 
+// ---- simulation-driver helpers (src/config.cpp, src/array_and_matrix_operations.cpp:121-256) ----
+int qldpc_sort_permutation(const double *keys, int32_t n, int32_t *perm_out) {
+    if (n < 0 || (n > 0 && (!keys || !perm_out))) return fail(QLDPC_EINVAL, "bad n / NULL arrays");
+    // The reference sorts config structs by code_rate with std::sort (not
+    // stable): the same libstdc++ algorithm on the same key sequence moves the
+    // elements identically, so the permutation of (key, index) pairs is theirs.
+    std::vector<std::pair<double, int32_t>> v(n);
+    for (int32_t i = 0; i < n; ++i) v[i] = {keys[i], i};
+    std::sort(v.begin(), v.end(), [](const std::pair<double, int32_t> &a, const std::pair<double, int32_t> &b) {
+        return a.first < b.first;
+    });
+    for (int32_t i = 0; i < n; ++i) perm_out[i] = v[i].second;
+    return QLDPC_OK;
+}
+
+int qldpc_bits_to_remove(int32_t n, int32_t m, const int32_t *col_ptr, const int32_t *row_idx, int32_t n_punct,
+                         const int32_t *punctured, int32_t n_short, const int32_t *shortened, int32_t rate_adapt,
+                         int32_t *out, int32_t *count) {
+    if (n <= 0 || m < 0 || !col_ptr || !row_idx || !count || (n_punct && !punctured) || (n_short && !shortened))
+        return fail(QLDPC_EINVAL, "bad arguments");
+    // find_available_index over a marked-check bitmap (same first-unmarked choice
+    // as std::find over the marked list, in O(E) overall).
+    std::vector<char> marked(m, 0);
+    auto take = [&](int i) -> bool {
+        for (int e = col_ptr[i]; e < col_ptr[i + 1]; ++e)
+            if (!marked[row_idx[e]]) {
+                marked[row_idx[e]] = 1;
+                return true;
+            }
+        return false;
+    };
+    std::vector<int> removed;
+    std::vector<std::pair<int, int>> cand;  // (bit, column weight)
+    if (rate_adapt) {  // get_bits_positions_to_remove_rate_adapt (:189-256)
+        int s = 0, p = 0;
+        for (int i = 0; i < n; ++i) {
+            if (s < n_short && shortened[s] == i) {
+                removed.push_back(i);
+                ++s;
+            } else if (p < n_punct && punctured[p] == i) {
+                removed.push_back(i);
+                take(i);
+                ++p;
+            } else {
+                cand.push_back({i, col_ptr[i + 1] - col_ptr[i]});
+            }
+        }
+    } else {  // get_bits_positions_to_remove (:138-185)
+        for (int i = 0; i < n; ++i) cand.push_back({i, col_ptr[i + 1] - col_ptr[i]});
+    }
+    // std::sort by column weight (not stable): same algorithm, same order as the reference
+    std::sort(cand.begin(), cand.end(),
+              [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a.second < b.second; });
+    for (const auto &c : cand)
+        if (take(c.first)) removed.push_back(c.first);
+    std::sort(removed.begin(), removed.end());
+    *count = (int32_t)removed.size();
+    if (out) std::copy(removed.begin(), removed.end(), out);
+    return QLDPC_OK;
+}
+
 // ---- trial generator (src/simulation.cpp:540-551,713-719,743) ----------------
 int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_out) {
     if (count < 0 || (count > 0 && !seeds_out)) return fail(QLDPC_EINVAL, "bad count / NULL seeds_out");
