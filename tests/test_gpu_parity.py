@@ -330,3 +330,30 @@ def test_cpp_mirror_kat(gpu_available):
     exe = f"{ROOT}/qkd_ldpc_v_amd/host/host_mirror_check"
     r = subprocess.run([exe, "kat", matrix_path("kat_n6_m4.dense")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "iterations=1 syndromes_match=1 keys_match=1", r.stdout
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_nonfinite_and_consistent_frames(gpu_available, alg, prim, sec):
+    """Edge inputs: NaN / +-inf channel LLRs in some frames (NaN survives the
+    clip), frames whose channel decision already satisfies the
+    syndrome (Bob == Alice), and an all-zero key."""
+    H = load_fixture("c2_n10240_m2201.alist")
+    a, b, llr, s = frames(H, 0.02, 8, 90 + alg)
+    llr[0, 5] = np.nan
+    llr[1, 7] = np.inf
+    llr[2, 9] = -np.inf
+    llr[3, [11, 12, 13]] = [np.nan, np.inf, -np.inf]
+    lp = Q.log_p(0.02)
+    llr[4] = np.where(a[4] != 0, -lp, lp)  # consistent frame
+    llr[5] = lp                             # all-zero key, zero syndrome
+    s[5] = 0
+    assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0, batch=8, llr=llr, synd=s)
+
+
+def test_zero_batch_and_single_frame(gpu_available):
+    H = load_fixture("c1_n1024_m220.alist")
+    g = graph("c1_n1024_m220.alist")
+    _, _, llr, s = frames(H, 0.02, 1, 3)
+    out = g.decode(Q.Params(Q.SPA, 50, True, 100.0), llr[:0], s[:0])
+    assert out.bits.shape == (0, H.n)
+    assert_parity("c1_n1024_m220.alist", Q.SPA, 0, 0, qber=0, batch=1, llr=llr, synd=s)
