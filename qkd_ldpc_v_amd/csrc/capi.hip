@@ -278,7 +278,7 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         if (row_ptr[j + 1] == row_ptr[j]) return false;  // empty rows: v1 checks them by row-ELL
     const long long E = g.E;
     const int forced = env_int("QLDPC_V2_WAVES", 0);
-    const int shapes[3][2] = {{V2_R_SMALL, 0}, {V2_R_MID, 0}, {V2_R_SMALL, V2_RG_HYBRID}};
+    const int shapes[4][2] = {{V2_R_TIGHT, 0}, {V2_R_SMALL, 0}, {V2_R_MID, 0}, {V2_R_SMALL, V2_RG_HYBRID}};
     for (const auto &sh : shapes) {
         const int R = sh[0] + sh[1];  // slots per lane
         const int wmax = v2_threads_for(sh[0]) / 64;
@@ -657,6 +657,11 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.ell_col = dg->ell_col; a.row_deg = dg->row_deg;
     a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
     a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
+    {
+        const double lim = (a.thr_on && p->thr < 44.0) ? p->thr : 44.0;
+        a.spa_tlim = std::tanh(lim / 2.);
+        a.spa_ctop = 2. * std::atanh(0x1.fffffffffffffp-1);
+    }
     a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
     a.frame_counter = w->counter;
     a.scratch = w->scratch;

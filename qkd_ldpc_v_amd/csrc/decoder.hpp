@@ -30,7 +30,7 @@ enum Variant : int {
 // Register slots per lane of the V2 instantiations.  (A third, 84 slots x 8
 // waves, holds no more edges than 56 x 12 and its SPA build falls back to a
 // scratch array, so it is not built.)
-constexpr int V2_R_SMALL = 44, V2_R_MID = 56;
+constexpr int V2_R_TIGHT = 40, V2_R_SMALL = 44, V2_R_MID = 56;
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;
 // Workgroup size each V2 instantiation is compiled for (its VGPR budget).
@@ -58,6 +58,9 @@ struct DecodeArgs {
     // decoder parameters
     int alg, max_it, thr_on;
     double thr, primary, secondary;
+    // SPA edge-form constants, computed by the host C library (capi.hip):
+    double spa_tlim;  // tanh(min(thr, 44) / 2.)  (1 when clipping is off)
+    double spa_ctop;  // 2. * atanh(1 - 2^-53)
     // frames
     int batch;
     const double *llr;      // [batch][n]

@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
     // threshold_matrix disabled == clipping at +inf (|v| > inf never holds; NaN passes)
     const double thr = a.thr_on ? a.thr : __builtin_inf();
+    const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
     const V2Layout L(n, m, nc, T, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
@@ -145,7 +146,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
         int iters = a.max_it, okv = 0;
         bool had_vn = false;
+        if constexpr (ALG == 0) {
+#pragma unroll
+            for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
+        }
         for (int it = 0;; ++it) {
+            // SPA: iteration 0's b2c is the unclipped channel LLR (:21-29)
+            const double lim_it = had_vn ? lim : 44.0;
+            const double tlim_it = had_vn ? a.spa_tlim : 1.0;  // tanh(22) = 1
             const bool check = ADAPT ? (it < a.max_it) : (it > 0);
             const bool compute = it < a.max_it;
             ++epoch;
@@ -166,21 +174,31 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const double tv = total[col];
                 const int zb = (tv <= 0.0) ? 1 : 0;
                 if (k < KT) zt |= (uint32_t)zb << k;
-                double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
-                if (had_vn) {
-                    x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
-                }
                 const bool start = (mt & META_START) != 0;
                 const int s = (int)(sm & 1u);
-                if constexpr (SPA_FAM) {
+                if constexpr (ALG == 0) {
+                    // b2c = total - c2b (:115); c2b is +0 in iteration 0, so b = the
+                    // channel LLR exactly there, and the clip (:122-123) is folded
+                    // into tanh_half_clip with the iteration's (lim, thr).
+                    const double b = tv - c2b.get(k);
+                    double t = b;
+                    if (compute) t = ql_exact::tanh_half_clip(b, lim_it, tlim_it);  // tanh(b2c / 2.) (:60)
+                    c2b.set(k, t);
+                    const double st = (s ? -1. : 1.) * t;  // (:57-62)
+                    acc = start ? st : acc * t;
+                } else if constexpr (SPA_FAM) {
+                    double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
+                    if (had_vn) x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
                     double t = x;
-                    if (compute) t = (ALG == 0) ? ql_exact::tanh_dec(x / 2.) : tanh_lin(x / 2.);
+                    if (compute) t = tanh_lin(x / 2.);
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
                 } else {
+                    double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
+                    if (had_vn) x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
                     c2b.set(k, x);
-                    if (!SPA_FAM && k < KT && k > 0) {
+                    if (k < KT && k > 0) {
                         // the first START closes the tail segment: keep its aggregate
                         if (k == head) {
                             tailagg[tid] = make_double2(m1, m2);
@@ -260,9 +278,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             auto message = [&](int k, uint32_t mt, uint32_t mt2) {
                 if (k > 0) r += (mt & META_START) ? 1 : 0;
                 double c;
-                if constexpr (SPA_FAM) {
+                if constexpr (ALG == 0) {
+                    // 2. * atanh(rp / t) (:66-68) and the clip (:73-74) in one
+                    c = ql_exact::atanh2_clip(rowA[r] / c2b.get(k), thr, a.spa_ctop);
+                } else if constexpr (SPA_FAM) {
                     const double prod = rowA[r] / c2b.get(k);  // :66
-                    c = 2. * ((ALG == 0) ? ql_exact::atanh_dec(prod) : atanh_lin(prod));
+                    c = 2. * atanh_lin(prod);
                 } else {
                     const double x = c2b.get(k);
                     const double2 ab = rowAB[r];
@@ -280,7 +301,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         c = prod * ((d < 0.) ? 0. : d);
                     }
                 }
-                c = clip_msg(c, thr);  // (:73-74)
+                if constexpr (ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 c2b.set(k, c);
                 const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
                 if (kp == 0) {
@@ -418,6 +439,7 @@ KernelFn pick_v2(int alg) {
 
 KernelFn kernel_v2(int R, int RG, int alg) {
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
+    if (R == V2_R_TIGHT) return pick_v2<V2_R_TIGHT, 0>(alg);
     if (R == V2_R_SMALL) return pick_v2<V2_R_SMALL, 0>(alg);
     return pick_v2<V2_R_MID, 0>(alg);
 }

@@ -568,4 +568,218 @@ QL_HD double atanh_dec(double x) {
     return t;
 }
 
+
+// ---------------------------------------------------------------------------
+// Edge forms (what the SPA kernel calls): the reference's two per-edge calls
+// with their scalings folded in, `tanh(b / 2.)` (src/qkd_ldpc_algorithm.cpp:60)
+// and `2. * atanh(p)` (:68).  Same IEEE operations as tanh_dec / atanh_dec on
+// every input; what changes is how the cases are combined:
+//   * the expm1 reconstructions of every k class tanh can reach are one
+//     expression, y = add_exponent((xr - (e2 + X3)) + X4, k) + B, with the
+//     per-class constants X3, X4, B selected by integer ops (derivation below);
+//   * the rare inputs (tiny, |x| >= 22, inf, NaN; atanh's |p| >= 1 - 2^-21,
+//     |p| < 2^-28) are recomputed by the full restatement in a branch the
+//     wave only enters when one of its lanes needs it (QL_RARE);
+//   * b / 2 is never formed on the common path: |b| = 2|x| is the expm1
+//     argument magnitude itself; 2 * copysign(0.5 * y, p) == copysign(y, p).
+// A divergent `if` on a rare lane condition: the wave skips the body (exec
+// empty) unless one of its lanes needs it.  QL_COUNT_COMMON drops the rare
+// bodies — for instruction counting only, never in a product build.
+#if defined(QL_COUNT_COMMON)
+#define QL_RARE(c) if (false)
+#else
+#define QL_RARE(c) if (__builtin_expect((c), 0))
+#endif
+
+// tanh(b / 2.) bit-identical to glibc.  Common path: 2^-54 <= |b| < 44 (that
+// is 2^-55 <= |x| < 22 for x = b/2, computed exactly as |b|/2).
+//
+// expm1(u), u = +-|b|, reconstructions of s_expm1.c with D = xr - e2:
+//   k = 0        xr - (xr*e - hxs)             == D              (c = +0 here)
+//   k = -1       0.5*(xr - e2) - 0.5           == add_exp(D + -1, -1)
+//                 (0.5*D exact, and RN commutes with scaling by 2^-1)
+//   k <= -2, k > 56   add_exp(1 - (e2 - xr), k) - 1 == add_exp(D + 1, k) + -1
+//   2 <= k < 20  add_exp((1 - 2^-k) - (e2 - xr), k) == add_exp(D + tb, k)
+//   20 <= k <= 56  add_exp((xr - (e2 + 2^-k)) + 1, k)
+// (a - (e2 - xr) == a + (xr - e2) bitwise for a != 0; e2 + -0 == e2; y + -0 == y).
+// k = 1 and k = 1024 are unreachable (u in (-2, 0] or [2, 44)).
+// tanh tail: z = C + num / (y + 2) with (x > 0 shown; x < 0 negates C, num)
+//   |x| < 1:  C = -0, num = -y        (z = -y/(y+2))
+//   |x| >= 1: C = 1,  num = -2        (z = 1 - 2/(y+2))
+QL_HD double tanh_half_full(double b) { return tanh_dec(b / 2.); }
+
+// Common path of tanh(b / 2.); *ib = hi word of |b|.  Exact for
+// 2^-54 <= |b| < 44; other lanes get a don't-care value.
+QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double Q1 = -3.33333333333331316428e-02, Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05, Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+
+    const uint32_t jb = hi_word(b);
+    const uint32_t ib = jb & 0x7fffffffu;         // hi word of |b| = 2|x|
+    const uint32_t sx = jb & 0x80000000u;
+    const bool big = ib >= 0x40000000u;            // |x| >= 1
+    const double ab = __builtin_fabs(b);
+    const double u = big ? ab : -ab;
+    double kf = invln2 * u + (big ? 0.5 : -0.5);
+#if !defined(__HIP_DEVICE_COMPILE__)
+    kf = (kf > 1e6 || kf < -1e6 || kf != kf) ? 0.0 : kf;  // host: keep the cast defined on special lanes
+#endif
+    int32_t k = (ib < 0x3FF0A2B2u) ? -1 : (int32_t)kf;   // only u < 0 reaches |u| < 1.5 ln2
+    k = (ib > 0x3fd62e42u) ? k : 0;
+    const double t = (double)k;
+    const double hi = u - t * ln2_hi;
+    const double lo = t * ln2_lo;
+    const double xr = hi - lo;
+    const double c = (hi - xr) - lo;
+    const double hfx = 0.5 * xr;
+    const double hxs = xr * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t3 = 3.0 - r1 * hfx;
+    const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
+    const double e2 = (xr * (e - c) - c) - hxs;
+    // per-class constants (all with a zero low word)
+    const uint32_t ku = (uint32_t)k;
+    const bool fcls = (ku - 20u) <= 36u;           // 20 <= k <= 56
+    const bool far = (ku + 1u) > 57u;              // k <= -2 or k > 56
+    uint32_t a_hi = 0x3ff00000u - (0x200000u >> (ku & 31u));   // 1 - 2^-k; 1 when far
+    a_hi = (k == 0) ? 0x80000000u : a_hi;          // -0
+    a_hi = (k == -1) ? 0xbff00000u : a_hi;         // -1
+    const double X3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);  // 2^-k or -0
+    const double X4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
+    const double B = from_words(far ? 0xbff00000u : 0x80000000u, 0u);                 // -1 or -0
+    const double y = add_exponent((xr - (e2 + X3)) + X4, k) + B;
+    const double num = big ? from_words(0xc0000000u ^ sx, 0u) : from_words(hi_word(y) ^ 0x80000000u ^ sx, lo_word(y));
+    const double C = from_words(big ? (0x3ff00000u ^ sx) : 0x80000000u, 0u);
+    *ib_out = ib;
+    return C + div_rn_safe(num, y + 2.0);
+}
+
+QL_HD double tanh_half_dec(double b) {
+    uint32_t ib;
+    double z = tanh_half_common(b, &ib);
+    const bool special = (ib - 0x3c900000u) >= (0x40460000u - 0x3c900000u);  // tiny, |x| >= 22, inf, NaN
+    QL_RARE(special) z = tanh_half_full(b);
+    return z;
+}
+
+// The reference's threshold_matrix on one value (src/array_and_matrix_operations.cpp:962-969):
+// |v| > thr -> +-thr, NaN passes; thr = +inf disables it.
+QL_HD double clip_thr(double v, double thr) { return (__builtin_fabs(v) > thr) ? __builtin_copysign(thr, v) : v; }
+
+// tanh(clip_thr(b, thr) / 2.) with lim = min(thr, 44) and t_lim = glibc
+// tanh(lim / 2.) (host-computed; 1 for lim = 44).  For |b| >= lim the result is
+// +-t_lim clipped or not (|b| > thr clips to +-thr, and tanh(+-x) = +-1 for
+// |x| >= 22), so the clip only matters on lanes the rare branch takes; its body
+// is the three cases glibc's s_tanh.c returns early on, inline:
+//   |x| < 2^-55: x*(1+x);  NaN: x+x;  else +-t_lim.   (x = b / 2.)
+QL_HD double tanh_half_clip(double b, double lim, double t_lim) {
+    uint32_t ib;
+    double z = tanh_half_common(b, &ib);
+    const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);  // tiny, |b| >= lim, NaN
+    QL_RARE(special) {
+        const double x = b / 2.;
+        z = (ib < 0x3c900000u) ? x * (1.0 + x) : __builtin_copysign(t_lim, b);
+        z = (b != b) ? x + x : z;
+    }
+    return z;
+}
+
+// 2 * atanh(p) bit-identical to 2. * glibc atanh.  Common path:
+// 2^-28 <= |p| < 1 - 2^-21 (log1p argument a in [2^-27, 2^22): finite, u0 = 1 + a).
+QL_HD double atanh2_full(double p) { return 2. * atanh_dec(p); }
+
+// Common path of 2. * atanh(p); *ia = hi word of |p|.  Exact for
+// 2^-28 <= |p| < 1 - 2^-21; other lanes get a don't-care value.
+QL_HD double atanh2_common(double p, uint32_t *ia_out) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01;
+    const double Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01;
+    const double Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01;
+    const double Lp7 = 1.479819860511658591e-01;
+
+    const double xa = __builtin_fabs(p);
+    const uint32_t ia = hi_word(xa);
+    const bool smallx = ia < 0x3fe00000u;          // |p| < 0.5
+    const double twoxa = xa + xa;
+    const double qd = div_rn_safe(smallx ? twoxa * xa : twoxa, 1.0 - xa);
+    const double a = smallx ? twoxa + qd : qd;
+    // --- log1p(a) core, a in [2^-27, 2^22) ---
+    const bool k0 = hi_word(a) < 0x3FDA827Au;      // a < 0.41422: f = a, k = 0, c = 0
+    const double u0 = 1.0 + a;
+    int32_t hu = (int32_t)hi_word(u0);
+    int32_t k = (hu >> 20) - 1023;                 // >= 0
+    const double cn = (k > 0) ? 1.0 - (u0 - a) : a - (u0 - 1.0);
+    double c = div_rn_safe(cn, u0);
+    hu &= 0x000fffff;
+    const bool up = hu >= 0x6a09e;
+    const double u = with_hi_word(u0, (uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)));
+    k = up ? k + 1 : k;
+    hu = up ? (0x00100000 - hu) >> 2 : hu;
+    double f = u - 1.0;
+    f = k0 ? a : f;
+    k = k0 ? 0 : k;
+    hu = k0 ? 1 : hu;
+    c = k0 ? 0.0 : c;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    const double s = div_rn_safe(f, 2.0 + f);
+    const double z = s * s;
+    const double R1 = z * Lp1;
+    const double z2 = z * z;
+    const double R2 = Lp2 + z * Lp3;
+    const double z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5;
+    const double z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    // k == 0 through the k != 0 formula (dk = c = 0): see atanh_dec
+    double y = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    QL_RARE(hu == 0) {                             // |f| < 2^-20
+        const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+        const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
+        const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+        y = (f == 0.0) ? yzero : ysmall;
+    }
+    *ia_out = ia;
+    return __builtin_copysign(y, p);               // 2 * copysign(0.5 * y, p)
+}
+
+QL_HD double atanh2_dec(double p) {
+    uint32_t ia;
+    double r = atanh2_common(p, &ia);
+    const bool special = (ia - 0x3e300000u) >= (0x3fefffffu - 0x3e300000u);  // tiny, >= 1 - 2^-21, NaN
+    QL_RARE(special) r = atanh2_full(p);
+    return r;
+}
+
+// clip_thr(2. * atanh(p), thr).  atanh2_common is exact for 2^-28 <= |p| <
+// 1 - 2^-53 (the log1p argument stays below 2^53); its result is below 37.5 in
+// magnitude and never NaN, so its clip is one compare.  The rare branch holds
+// e_atanh.c's early returns and the one value left, |p| = 1 - 2^-53, whose
+// 2*atanh is the constant c_top (host-computed by glibc):
+//   |p| < 2^-28: 2*p;  |p| = 1: +-inf;  |p| > 1 or NaN: NaN.
+QL_HD double atanh2_clip(double p, double thr, double c_top) {
+    uint32_t ia;
+    double r = atanh2_common(p, &ia);
+    const double xa = __builtin_fabs(p);
+    const bool special = (ia < 0x3e300000u) || !(xa < 0x1.fffffffffffffp-1);  // tiny, >= 1 - 2^-53, NaN
+    QL_RARE(special || __builtin_fabs(r) > thr) {
+        double v = (xa == 1.0) ? __builtin_copysign(__builtin_inf(), p) : __builtin_copysign(c_top, p);
+        v = (ia < 0x3e300000u) ? 2. * p : v;
+        v = (xa > 1.0 || p != p) ? 2. * ((p - p) / (p - p)) : v;
+        r = clip_thr(special ? v : r, thr);
+    }
+    return r;
+}
+
 }  // namespace ql_exact

@@ -39,8 +39,8 @@ int main(int argc, char **argv) {
     long per = argc > 1 ? atol(argv[1]) : 1000000;
     uint64_t seed0 = argc > 2 ? strtoull(argv[2], 0, 10) : 12345;
     unsigned nt = std::thread::hardware_concurrency(); if (!nt) nt = 4;
-    const char *names[10] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec"};
-    std::atomic<long> bad[10]; for (auto &b : bad) b = 0;
+    const char *names[14] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec", "tanh_half_dec", "atanh2_dec", "tanh_half_clip", "atanh2_clip"};
+    std::atomic<long> bad[14]; for (auto &b : bad) b = 0;
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] {
         uint64_t s = seed0 * 1000003 + t;
@@ -59,15 +59,31 @@ int main(int argc, char **argv) {
             if (!same(ql_exact::tanh_dec(x), std::tanh(x))) { if (bad[8]++ < 5) printf("tanh_dec  x=%a got=%a ref=%a\n", x, ql_exact::tanh_dec(x), std::tanh(x)); }
             if (!same(ql_exact::atanh_dec(y), std::atanh(y))) { if (bad[9]++ < 5) printf("atanh_dec x=%a got=%a ref=%a\n", y, ql_exact::atanh_dec(y), std::atanh(y)); }
             if (!same(ql_exact::log1p_bf(x), std::log1p(x))) { if (bad[7]++ < 5) printf("log1p_bf x=%a got=%a ref=%a\n", x, ql_exact::log1p_bf(x), std::log1p(x)); }
+            // edge forms: tanh(b / 2.) and 2. * atanh(p), on b in the decoder's +-100 and on p near +-1
+            const double b = (mode == 1) ? x * (100.0 / 60.0) : x;
+            if (!same(ql_exact::tanh_half_dec(b), std::tanh(b / 2.))) { if (bad[10]++ < 5) printf("tanh_half_dec b=%a got=%a ref=%a\n", b, ql_exact::tanh_half_dec(b), std::tanh(b / 2.)); }
+            if (!same(ql_exact::atanh2_dec(y), 2. * std::atanh(y))) { if (bad[11]++ < 5) printf("atanh2_dec p=%a got=%a ref=%a\n", y, ql_exact::atanh2_dec(y), 2. * std::atanh(y)); }
+            // clipped forms at the shipped threshold (100), a small one (10) and off (inf)
+            {
+                const double T = (i % 3 == 0) ? 100.0 : (i % 3 == 1) ? 10.0 : HUGE_VAL;
+                const double lim = T < 44.0 ? T : 44.0;
+                const double rt = std::tanh(ql_exact::clip_thr(b, T) / 2.);
+                if (!same(ql_exact::tanh_half_clip(b, lim, std::tanh(lim / 2.)), rt)) { if (bad[12]++ < 5) printf("tanh_half_clip b=%a T=%g got=%a ref=%a\n", b, T, ql_exact::tanh_half_clip(b, lim, std::tanh(lim / 2.)), rt); }
+                const double Ta = (i % 3 == 0) ? 100.0 : (i % 3 == 1) ? 3.0 : HUGE_VAL;
+                const double ra = ql_exact::clip_thr(2. * std::atanh(y), Ta);
+                if (!same(ql_exact::atanh2_clip(y, Ta, 2. * std::atanh(0x1.fffffffffffffp-1)), ra)) { if (bad[13]++ < 5) printf("atanh2_clip p=%a T=%g got=%a ref=%a\n", y, Ta, ql_exact::atanh2_clip(y, Ta, 2. * std::atanh(0x1.fffffffffffffp-1)), ra); }
+            }
         }
     });
     for (auto &x : th) x.join();
     long tot = 0;
-    for (int f = 0; f < 10; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
+    for (int f = 0; f < 14; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
     // Sweep the high words around every branch boundary of the four functions.
     const uint32_t bounds[] = {0x3FDA827A, 0xbfd2bec3, 0xbfd2bec4, 0x3e200000, 0x3c900000, 0x43400000, 0x3ff00000,
                                0x3fd62e42, 0x3FF0A2B2, 0x4043687A, 0x40862E42, 0x40360000, 0x3c800000, 0x3fe00000,
-                               0x3ff6a09e, 0x3fe6a09e, 0x3e300000, 0x7ff00000};
+                               0x3ff6a09e, 0x3fe6a09e, 0x3e300000, 0x7ff00000,
+                               // edge forms (thresholds on b = 2x and on p)
+                               0x40000000, 0x40460000, 0x3fefffff, 0x3fe00000, 0x3FE62E42, 0x4000A2B2, 0x40590000};
     long bb = 0, nb = 0;
     for (uint32_t base : bounds)
         for (int d = -300; d <= 300; ++d)
@@ -76,18 +92,43 @@ int main(int argc, char **argv) {
                     const uint32_t hi = (base + d) ^ (sg ? 0x80000000u : 0u);
                     const uint64_t b = ((uint64_t)hi << 32) | lo;
                     double x; memcpy(&x, &b, 8);
-                    const double r[10] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
+                    const double r[14] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
                                          std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
-                                         std::tanh(x), std::atanh(x)};
-                    const double g[10] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
+                                         std::tanh(x), std::atanh(x), std::tanh(x / 2.), 2. * std::atanh(x),
+                                         std::tanh(ql_exact::clip_thr(x, 100.0) / 2.),
+                                         ql_exact::clip_thr(2. * std::atanh(x), 100.0)};
+                    const double g[14] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
                                          ql_exact::log1p_exact(x), ql_exact::tanh_bf(x), ql_exact::atanh_bf(x),
                                          ql_exact::expm1_bf(x), ql_exact::log1p_bf(x), ql_exact::tanh_dec(x),
-                                         ql_exact::atanh_dec(x)};
-                    for (int f = 0; f < 10; ++f) {
+                                         ql_exact::atanh_dec(x), ql_exact::tanh_half_dec(x), ql_exact::atanh2_dec(x),
+                                         ql_exact::tanh_half_clip(x, 44.0, std::tanh(22.0)), ql_exact::atanh2_clip(x, 100.0, 2. * std::atanh(0x1.fffffffffffffp-1))};
+                    for (int f = 0; f < 14; ++f) {
                         ++nb;
                         if (!same(r[f], g[f]) && bb++ < 5) printf("boundary %s x=%a ref=%a got=%a\n", names[f], x, r[f], g[f]);
                     }
                 }
+    // explicit edge values of the clipped edge forms (x and -x, three thresholds)
+    {
+        const double C_TOP = 2. * std::atanh(0x1.fffffffffffffp-1);
+        const double vals[] = {0.0, 0x1p-1074, 0x1p-1022, 0x1p-60, 0x1p-55, 0x1p-54, 0x1.fffffffffffffp-55, 0x1p-29,
+                               0x1p-28, 0x1.fffffffffffffp-29, 0.5, 0x1.fffffffffffffp-2, 1.0, 0x1.fffffffffffffp-1,
+                               0x1.ffffffffffffep-1, 0x1.ffffffffffffdp-1, 1.0 - 0x1p-21, 1.0 - 0x1p-22, 0x1.0000000000001p+0,
+                               2.0, 3.0, 10.0, 43.999999999999993, 44.0, 44.000000000000007, 99.99999999999999, 100.0,
+                               100.00000000000001, 1e300, 1.7976931348623157e308, HUGE_VAL, NAN};
+        for (double v0 : vals)
+            for (int sg = 0; sg < 2; ++sg)
+                for (double T : {100.0, 10.0, 3.0, (double)HUGE_VAL}) {
+                    const double v = sg ? -v0 : v0;
+                    const double lim = T < 44.0 ? T : 44.0;
+                    const double rt = std::tanh(ql_exact::clip_thr(v, T) / 2.);
+                    const double gt = ql_exact::tanh_half_clip(v, lim, std::tanh(lim / 2.));
+                    const double ra = ql_exact::clip_thr(2. * std::atanh(v), T);
+                    const double ga = ql_exact::atanh2_clip(v, T, C_TOP);
+                    nb += 2;
+                    if (!same(rt, gt) && bb++ < 20) printf("edge tanh_half_clip v=%a T=%g ref=%a got=%a\n", v, T, rt, gt);
+                    if (!same(ra, ga) && bb++ < 20) printf("edge atanh2_clip v=%a T=%g ref=%a got=%a\n", v, T, ra, ga);
+                }
+    }
     printf("boundary mismatches: %ld / %ld\n", bb, nb);
     return (tot || bb) ? 1 : 0;
 }
