@@ -76,6 +76,7 @@ struct DeviceGraph {
     int32_t *lane_nst = nullptr, *lane_epl = nullptr;
     uint32_t *slot_meta_ms = nullptr;                  // V2 min-sum: rows listed by kpos
     uint64_t *vn_mask = nullptr, *vn_mask_ms = nullptr; // V2: [wave][dv_max] slot masks
+    uint64_t *vn_exec = nullptr, *vn_exec_ms = nullptr; // V2: [wave][dv_max][slot] lane masks
     uint32_t *slot_meta2 = nullptr, *slot_meta2_ms = nullptr;  // V2 hybrid: stage index per slot
     int32_t *hd_bits = nullptr, *hd_dv = nullptr, *stage_off = nullptr;
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
@@ -440,11 +441,13 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         g->stage_doubles = off;
     }
     g->n_hd = (int)hd_bits.size();
+    const int S4 = G4 * 4;  // V2 slots per lane (register + scratch)
     auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm,
-                          std::vector<uint32_t> &mt2) -> int {
+                          std::vector<uint32_t> &mt2, std::vector<uint64_t> &vex) -> int {
         mt.assign((size_t)G4 * TS * 4, 0);
         mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
+        vex.assign(v2 ? (size_t)W * g->dv_max * S4 : 0, 0);
         perm = ledge;
         if (sorted)
             for (int j = 0; j < m; ++j)
@@ -477,7 +480,10 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         const int j = lrow[e];
                         const int ed = perm[e];  // the edge at that position
                         wd = (uint32_t)col_idx[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
-                        if (v2) vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
+                        if (v2) {
+                            vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
+                            vex[((size_t)w * g->dv_max + kpos[ed]) * S4 + k] |= 1ull << li;
+                        }
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
                             mt2[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] =
                                 (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
@@ -498,9 +504,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     };
     std::vector<int32_t> row_orig(v2 ? g->row_order : std::vector<int>());
     std::vector<uint32_t> meta_ms, meta2, meta2_ms;
-    std::vector<uint64_t> vnm, vnm_ms;
-    int brc = build_meta(false, meta, vnm, meta2);
-    if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms, meta2_ms);
+    std::vector<uint64_t> vnm, vnm_ms, vex, vex_ms;
+    int brc = build_meta(false, meta, vnm, meta2, vex);
+    if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms, meta2_ms, vex_ms);
     if (brc) return brc;
     if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
         auto visited = [&](const std::vector<uint64_t> &v) {
@@ -548,6 +554,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         int rc;
         if ((rc = upload(&dg->slot_meta, meta)) || (rc = upload(&dg->slot_meta_ms, meta_ms)) ||
             (rc = upload(&dg->vn_mask, vnm)) || (rc = upload(&dg->vn_mask_ms, vnm_ms)) ||
+            (rc = upload(&dg->vn_exec, vex)) || (rc = upload(&dg->vn_exec_ms, vex_ms)) ||
             (rc = upload(&dg->slot_meta2, meta2)) || (rc = upload(&dg->slot_meta2_ms, meta2_ms)) ||
             (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
             (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
@@ -654,6 +661,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.lane_nst = dg->lane_nst; a.lane_epl = dg->lane_epl;
     if (v2 && alg >= 2) a.slot_meta = dg->slot_meta_ms;
     a.vn_mask = (v2 && alg >= 2) ? dg->vn_mask_ms : dg->vn_mask;
+    a.vn_exec = (v2 && alg >= 2) ? dg->vn_exec_ms : dg->vn_exec;
     a.ell_col = dg->ell_col; a.row_deg = dg->row_deg;
     a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
     a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
@@ -807,6 +815,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->row_orig);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
+        (void)hipFree(d->vn_exec);
+        (void)hipFree(d->vn_exec_ms);
         (void)hipFree(d->lane_epl);
         (void)hipFree(d->ell_col);
         (void)hipFree(d->row_deg);

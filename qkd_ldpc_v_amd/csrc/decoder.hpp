@@ -84,6 +84,7 @@ struct DecodeArgs {
     int v2R;                 // register slots of the V2 instantiation to launch
     int v2RG;                // + slots in per-workgroup global scratch (0 or V2_RG_HYBRID)
     const uint64_t *vn_mask; // [waves][dv_max]: slots holding a kk-th bit edge, per wave
+    const uint64_t *vn_exec; // [waves][dv_max][slots]: lanes whose slot holds a kk-th bit edge
     // V2 hybrid: VN terms k >= vn_k0 are staged in scratch by the message pass
     // and summed per bit in one gather pass (bits sorted by degree, descending).
     int vn_k0;                      // first staged term (dv_max: none)

@@ -166,6 +166,9 @@ template <int R>
 struct MetaSrcW : MetaSrc<R> {
     template <typename F>
     __device__ __forceinline__ void each_upto(int epl_s, F &&f) const {
+        // opaque per call: keeps the slot guards scalar compares instead of
+        // 40 hoisted lane masks (which spill into VGPR lanes: 2 VALU per slot)
+        asm volatile("" : "+s"(epl_s));
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
             if (4 * g < epl_s) {
@@ -181,6 +184,7 @@ struct MetaSrcW : MetaSrc<R> {
     // of identical layout (rs2).
     template <typename F>
     __device__ __forceinline__ void each_upto2(int epl_s, __amdgpu_buffer_rsrc_t rs2, F &&f) const {
+        asm volatile("" : "+s"(epl_s));
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
             if (4 * g < epl_s) {
@@ -190,6 +194,20 @@ struct MetaSrcW : MetaSrc<R> {
                 if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1], (uint32_t)q2[1]);
                 if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2], (uint32_t)q2[2]);
                 if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3], (uint32_t)q2[3]);
+            }
+        }
+    }
+    // Groups of four slots at least one of which is in the mask: f(g, q, bits)
+    // with q the group's four metadata words and bits its 4-bit slice of the mask.
+    template <typename F>
+    __device__ __forceinline__ void each_group_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            const uint32_t w = (4 * g < 32) ? mlo : mhi;
+            const uint32_t bits = (w >> ((4 * g) & 31)) & 15u;
+            if (bits) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
+                f(g, q, bits);
             }
         }
     }

@@ -88,7 +88,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     meta.init(a.slot_meta, tid, T);
     // VN phase kk visits only the slots where some lane of this wave holds the
     // kk-th edge of a bit (capi.hip: vn_mask[wave][kk]).
-    const uint64_t *vn_mask = a.vn_mask + (size_t)(tid >> 6) * a.dv_max;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint64_t *vn_mask = a.vn_mask + (size_t)wave * a.dv_max;
+    // ... and per slot, the lanes whose edge there is a bit's kk-th: an exec
+    // mask loaded by the scalar unit (no per-lane kpos test).
+    // (constant address space: read-only for the kernel's lifetime, so the loads are s_load)
+    typedef const __attribute__((address_space(4))) uint64_t const_u64;
+    const const_u64 *vn_exec = (const const_u64 *)(a.vn_exec + (size_t)wave * a.dv_max * S);
     double *stage = a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.stage_wg_offset;
     // (only used by the GATHER instantiations)
     const __amdgpu_buffer_rsrc_t stage_rs =
@@ -304,7 +310,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if constexpr (ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 c2b.set(k, c);
                 const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-                if (kp == 0) {
+                if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
                     const int col = (int)(mt & META_COL_MASK);
                     total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
                 }
@@ -327,11 +333,19 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const uint64_t vm = vn_mask[kk];
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
                 const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
-                meta.each_masked(mlo, mhi, [&](int k, uint32_t mt) {
-                    if (((mt >> META_KPOS_SHIFT) & META_KPOS_MASK) == (uint32_t)kk) {
-                        const int col = (int)(mt & META_COL_MASK);
-                        total[col] = total[col] + c2b.get(k);
-                    }
+                const const_u64 *ex = vn_exec + (size_t)kk * S;
+                // Four slots at a time: the four totals are read together (every
+                // lane; a bit's kk-th edge is unique, so no two lanes of the
+                // phase write one column), then added and written back by the
+                // lanes whose edge there is a kk-th one.
+                meta.each_group_masked(mlo, mhi, [&](int g, auto q, uint32_t) {
+                    double tv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
+                            total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
                 });
                 __syncthreads();
             }
