@@ -34,9 +34,11 @@ STAMPLIB := $(PKG)/diag/libqkdldpc_hip.so
 stamps: $(STAMPLIB)
 $(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
+$(CSRC)/decoder_v2_st.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
+	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
-$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2.o $(CSRC)/trials.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
+$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
 	mkdir -p $(PKG)/diag
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 

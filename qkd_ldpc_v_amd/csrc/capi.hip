@@ -274,7 +274,7 @@ std::vector<std::vector<int>> balance_rows(const int32_t *row_ptr, int m, int W,
 // no V2 instantiation fits (v1 is used).
 bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
     // head <= 31 (tail parity in a 32-bit mask), dummy column id n < 2^20
-    if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
+    if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK || g.n > V2_CODES_CAP) return false;
     for (int j = 0; j < g.m; ++j)
         if (row_ptr[j + 1] == row_ptr[j]) return false;  // empty rows: v1 checks them by row-ELL
     const long long E = g.E;

@@ -35,18 +35,6 @@ using namespace dev;
 
 constexpr int CTRL_BYTES = 16;
 
-// Diagnostic build only (-DQL_PHASE_STAMPS): per-wave s_memtime accumulators
-// of every phase's work and barrier-wait time, written to DecodeArgs::stamps.
-#ifdef QL_PHASE_STAMPS
-#define STAMP(id)                                                \
-    do {                                                         \
-        const uint64_t _t = __builtin_amdgcn_s_memtime();        \
-        st_acc[id] += _t - st_last;                              \
-        st_last = _t;                                            \
-    } while (0)
-#else
-#define STAMP(id) ((void)0)
-#endif
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 

@@ -30,17 +30,24 @@ __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15
 
 // LDS of one frame.  total has n + 1 entries: total[n] is the column of the
 // dummy slots that pad every lane of a wave to the same slot count.
+// The palette, the per-bit palette indices and the totals sit at fixed
+// offsets, so their LDS addresses are instruction immediates (no base
+// register): codes hold up to V2_CODES_CAP bits (plan_v2 enforces n <= it).
+constexpr int V2_PAL_OFF = V2_CTRL;                    // 4 doubles
+constexpr int V2_CODES_OFF = V2_PAL_OFF + 32;          // one palette index byte per bit
+constexpr int V2_TOTAL_OFF = V2_CODES_OFF + V2_CODES_CAP;
+static_assert(V2_TOTAL_OFF % 16 == 0 && V2_TOTAL_OFF < 65536, "ds offset immediates are 16-bit");
 struct V2Layout {
     size_t total, rows, rowflag, tail, tailneg, codes, palette, bytes;
-    __host__ __device__ V2Layout(int n, int m, int nc, int T, bool minsum) {
-        size_t o = V2_CTRL;
+    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum) {
+        palette = V2_PAL_OFF;
+        codes = V2_CODES_OFF;
+        size_t o = V2_TOTAL_OFF;
         total = o; o = al16(o + (size_t)(n + 1) * 8);
         rows = o; o = al16(o + (size_t)m * (minsum ? 16 : 8));  // SPA: product; min-sum: {min1, min2}
-        palette = o; o = al16(o + 4 * 8);
         rowflag = o; o = al16(o + (minsum ? (size_t)m : 0));
         tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
         tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
-        codes = o; o = al16(o + (size_t)nc);
         bytes = o;
     }
 };
@@ -73,14 +80,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const V2Layout L(n, m, nc, T, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
-    double *total = reinterpret_cast<double *>(smem + L.total);
+    double *total = reinterpret_cast<double *>(smem + V2_TOTAL_OFF);
     double *rowA = reinterpret_cast<double *>(smem + L.rows);   // SPA
     double2 *rowAB = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
-    double *pal = reinterpret_cast<double *>(smem + L.palette);
+    double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
     uint8_t *rowflag = smem + L.rowflag;  // min-sum: bit0 syndrome, bit1 row mismatch, bit2 negative parity
     double2 *tailagg = reinterpret_cast<double2 *>(smem + L.tail);
     int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
-    uint8_t *codes = smem + L.codes;
+    uint8_t *codes = smem + V2_CODES_OFF;
 
     EdgeMsgsH<R, RG> c2b;
     c2b.bind(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles, tid);
@@ -112,10 +119,17 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const int up = (lane == 0) ? 0 : lane - 1;
     int epoch = 0;
     if (tid == 0) *s_flag = 0;
+#ifdef QL_PHASE_STAMPS
+    uint64_t st_acc[NUM_STAMPS];
+    for (int i = 0; i < NUM_STAMPS; ++i) st_acc[i] = 0;
+    uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
 
     for (;;) {
         if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        STAMP(ST_SETUP);
         __syncthreads();
+        STAMP(ST_SETUP_WAIT);
         const int f = *s_frame;
         if (f >= a.batch) break;
         const uint8_t *sy = a.synd + (size_t)f * m;
@@ -135,20 +149,30 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.llr + (size_t)f * n), (short)0, paletted ? 0 : n * 8, 0x00020000);
         {
+            // 2-bit codes -> one byte per bit (the message pass's llr lookup is
+            // then a byte read, no shift/mask arithmetic)
             const uint8_t *cs = a.codes + (size_t)f * nc;
-            for (int i = tid; i < nc; i += T) codes[i] = cs[i];
+            uint32_t *codes4 = reinterpret_cast<uint32_t *>(codes);
+            for (int i = tid; i < nc; i += T) {
+                const uint32_t b = cs[i];
+                codes4[i] = (b & 3u) | (((b >> 2) & 3u) << 8) | (((b >> 4) & 3u) << 16) | ((b >> 6) << 24);
+            }
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
         }
+        STAMP(ST_SETUP);
         __syncthreads();
+        STAMP(ST_SETUP_WAIT);
         auto llr_of = [&](int col) -> double {
-            if (paletted) return pal[(codes[col >> 2] >> ((col & 3) * 2)) & 3];
+            if (paletted) return pal[codes[col]];
             return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
         };
         // total starts as the channel LLRs: the check-node scan of iteration 0
         // reads the channel decision from it, and bits of degree 0 keep it.
         for (int i = tid; i < n; i += T) total[i] = llr_of(i);
         if (tid == 0) total[n] = 1.0;  // dummy column
+        STAMP(ST_SETUP);
         __syncthreads();
+        STAMP(ST_SETUP_WAIT);
 
         int iters = a.max_it, okv = 0;
         bool had_vn = false;
@@ -173,6 +197,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             // the first START are the tail of the previous lane's last row.
             int r = row0;
             int par = 0, cur_s = 0, mis = 0, neg = 0;
+            int div_unsafe = 0;
             uint32_t zt = 0;  // decisions of the first KT slots (tail parity)
             double acc = 1.0, m1 = DBL_MAX, m2 = DBL_MAX;
             meta.each_upto(epl, [&](int k, uint32_t mt) {
@@ -188,7 +213,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     // into tanh_half_clip with the iteration's (lim, thr).
                     const double b = tv - c2b.get(k);
                     double t = b;
-                    if (compute) t = ql_exact::tanh_half_clip(b, lim_it, tlim_it);  // tanh(b2c / 2.) (:60)
+                    if (compute) t = ql_exact::tanh_half_clip(b, lim_it, tlim_it, &div_unsafe);  // tanh(b2c / 2.) (:60)
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
@@ -230,6 +255,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     mis |= mr;
                     if constexpr (SPA_FAM) {
                         rowA[r] = acc;
+                        if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
                     } else {
                         rowAB[r] = make_double2(m1, m2);
                         rowflag[r] = (uint8_t)(cur_s | (mr << 1) | (neg << 2));
@@ -248,6 +274,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         for (int k = 0; k < KT; ++k)
                             if (k < head) p = p * c2b.get(k);
                         rowA[row0] = p;
+                        if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(p) >= 0x1p-900) ? 0 : 1;
                         mis |= ppar ^ hpar ^ s_row0;
                     }
                 } else {
@@ -270,8 +297,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
             }
             if (mis) *s_flag = epoch;
+            STAMP(ST_CN1);
             __syncthreads();
+            STAMP(ST_CN1_WAIT);
             const bool anymis = *s_flag == epoch;
+            // SPA: rp / t by div_rn_safe when every t of this wave came out of
+            // tanh's common path (|t| in [2^-55, 1]) and every row product of the
+            // wave is at least 2^-900 in magnitude: the operand range where the
+            // shortened Newton sequence is the IEEE quotient (exact_math.h).
+            const bool div_fast = (ALG == 0) && !__builtin_amdgcn_ballot_w64(div_unsafe != 0);
             if (check && !anymis) {
                 iters = ADAPT ? it + 1 : it;
                 okv = 1;
@@ -286,7 +320,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 double c;
                 if constexpr (ALG == 0) {
                     // 2. * atanh(rp / t) (:66-68) and the clip (:73-74) in one
-                    c = ql_exact::atanh2_clip(rowA[r] / c2b.get(k), thr, a.spa_ctop);
+                    const double ra = rowA[r], tk = c2b.get(k);
+                    double prod;  // :66
+                    if (div_fast) prod = ql_exact::div_rn_safe(ra, tk);
+                    else prod = ra / tk;
+                    c = ql_exact::atanh2_clip(prod, thr, a.spa_ctop);
                 } else if constexpr (SPA_FAM) {
                     const double prod = rowA[r] / c2b.get(k);  // :66
                     c = 2. * atanh_lin(prod);
@@ -327,7 +365,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
             }
+            STAMP(ST_CN3);
             __syncthreads();
+            STAMP(ST_VN0_WAIT);
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
             for (int kk = 1; kk < k0; ++kk) {
                 const uint64_t vm = vn_mask[kk];
@@ -347,7 +387,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
                             total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
                 });
+                STAMP(ST_VNK);
                 __syncthreads();
+                STAMP(ST_VNK_WAIT);
             }
             if constexpr (GATHER) {
                 // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
@@ -359,7 +401,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         for (int kk = k0; kk < dvb; ++kk) sacc = sacc + stage[a.stage_off[kk] + i];
                         total[b] = sacc;
                     }
+                    STAMP(ST_VNK);
                     __syncthreads();
+                    STAMP(ST_VNK_WAIT);
                 }
             }
             had_vn = true;
@@ -380,8 +424,16 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
         }
+        STAMP(ST_OUT);
         __syncthreads();
+        STAMP(ST_OUT_WAIT);
     }
+#ifdef QL_PHASE_STAMPS
+    if ((tid & 63) == 0 && a.stamps) {
+        uint64_t *dst = a.stamps + ((size_t)blockIdx.x * (a.T / 64) + (tid >> 6)) * NUM_STAMPS;
+        for (int i = 0; i < NUM_STAMPS; ++i) dst[i] = st_acc[i];
+    }
+#endif
 }
 
 // Palette + 2-bit codes of each frame's LLRs (one workgroup per frame).  Wave 0

@@ -681,7 +681,9 @@ QL_HD double clip_thr(double v, double thr) { return (__builtin_fabs(v) > thr) ?
 // |x| >= 22), so the clip only matters on lanes the rare branch takes; its body
 // is the three cases glibc's s_tanh.c returns early on, inline:
 //   |x| < 2^-55: x*(1+x);  NaN: x+x;  else +-t_lim.   (x = b / 2.)
-QL_HD double tanh_half_clip(double b, double lim, double t_lim) {
+// *tiny_or_nan is set (never cleared) when the result is NaN or below 2^-55
+// in magnitude: the only results outside [2^-55, 1] (see div_rn_safe's range).
+QL_HD double tanh_half_clip(double b, double lim, double t_lim, int *tiny_or_nan) {
     uint32_t ib;
     double z = tanh_half_common(b, &ib);
     const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);  // tiny, |b| >= lim, NaN
@@ -689,6 +691,7 @@ QL_HD double tanh_half_clip(double b, double lim, double t_lim) {
         const double x = b / 2.;
         z = (ib < 0x3c900000u) ? x * (1.0 + x) : __builtin_copysign(t_lim, b);
         z = (b != b) ? x + x : z;
+        if (ib < 0x3c900000u || b != b) *tiny_or_nan = 1;
     }
     return z;
 }
