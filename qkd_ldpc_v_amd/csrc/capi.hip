@@ -58,6 +58,11 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     uint8_t *codes = nullptr, *pal_ok = nullptr;
     double *palette = nullptr;
     size_t code_frames = 0;
+    // V2 split frames: group claim / publish / barrier / mismatch slots and the
+    // frames' totals, capacity in frames
+    int *split_ctl = nullptr;
+    double *gtotal = nullptr, *gstage = nullptr;
+    size_t split_frames = 0;
 };
 
 struct HostIO {  // device staging buffers of the host-buffer entry
@@ -80,6 +85,7 @@ struct DeviceGraph {
     uint32_t *slot_meta2 = nullptr, *slot_meta2_ms = nullptr;  // V2 hybrid: stage index per slot
     int32_t *hd_bits = nullptr, *hd_dv = nullptr, *stage_off = nullptr;
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
+    int32_t *part_row0 = nullptr; // V2 split: first layout row of each part
     int32_t *iso_bits = nullptr;
     std::mutex mu;
     std::map<void *, Workspace> ws;
@@ -142,6 +148,8 @@ struct qldpc_graph {
     std::vector<int> layout_row_ptr;        // V2: row_ptr of the rows in layout order
     int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
+    int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
+    std::vector<int> part_row0;             // V2 split: first layout row of each part (+ m)
     std::vector<std::unique_ptr<DeviceGraph>> devs;
 };
 
@@ -156,7 +164,13 @@ const char *variant_name(int v) {
     }
 }
 
+// Threads per workgroup: the graph's lanes, or one part's for split frames.
+int block_threads(const qldpc_graph &g) {
+    return (g.variant == VAR_V2 && g.split_k > 1) ? REG_TSTRIDE : g.T;
+}
+
 size_t lds_of(const qldpc_graph &g, int alg) {
+    if (g.variant == VAR_V2 && g.split_k > 1) return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true);
     return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T) : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
@@ -327,6 +341,70 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
     return false;
 }
 
+// V2 split plan, for codes whose frame does not fit one CU (totals beyond LDS
+// or more edges than 16 waves x 64 lanes x 40 slots): K parts of 16 waves
+// each (one workgroup per part, K <= 8 so a part group fits well inside one
+// XCD's 32 CUs), rows dealt to the 16K waves as in plan_v2 (contiguous
+// balanced blocks), part r = waves [16r, 16r + 16).  Totals go to global
+// memory.  QLDPC_SPLIT=0 disables it (v1 is used).
+bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr) {
+    if (env_int("QLDPC_SPLIT", 1) == 0) return false;
+    if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
+    for (int j = 0; j < g.m; ++j)
+        if (row_ptr[j + 1] == row_ptr[j]) return false;
+    const long long E = g.E;
+    const int R = V2_R_TIGHT, WP = REG_TSTRIDE / 64;
+    const long long cap_part = (long long)WP * 64 * R;
+    for (int K = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part); K <= 8; ++K) {
+        const int W = WP * K;
+        const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
+        if (cap > 64LL * R) continue;
+        std::vector<long long> sums;
+        const auto waves = balance_rows(row_ptr, g.m, W, cap, sums);
+        std::vector<int> order, rb(W + 1, 0), nrp(g.m + 1, 0);
+        for (int w = 0; w < W; ++w) {
+            order.insert(order.end(), waves[w].begin(), waves[w].end());
+            rb[w + 1] = (int)order.size();
+        }
+        for (int j = 0; j < g.m; ++j) nrp[j + 1] = nrp[j] + (row_ptr[order[j] + 1] - row_ptr[order[j]]);
+        int epl = 0;
+        bool ok = true;
+        for (int w = 0; w < W && ok; ++w) {
+            const long long ew = nrp[rb[w + 1]] - nrp[rb[w]];
+            if (ew == 0) continue;
+            const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
+            ok = e <= R;
+            epl = std::max(epl, e);
+            for (long long l = 0; l < 64 && ok; ++l) {
+                const long long e0 = nrp[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, nrp[rb[w + 1]]);
+                int starts = 0;
+                for (int j = rb[w]; j < rb[w + 1]; ++j)
+                    if (nrp[j] >= e0 && nrp[j] < e1) ++starts;
+                ok = starts <= 32;
+            }
+        }
+        if (!ok) continue;
+        std::vector<int> prow(K + 1);
+        int mrows = 0;
+        for (int r = 0; r <= K; ++r) prow[r] = rb[std::min(W, r * WP)];
+        for (int r = 0; r < K; ++r) mrows = std::max(mrows, prow[r + 1] - prow[r]);
+        if (lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true) > LDS_LIMIT) return false;
+        g.variant = VAR_V2;
+        g.v2R = R;
+        g.v2RG = 0;
+        g.T = W * 64;
+        g.EPL = epl;
+        g.wave_rows = rb;
+        g.row_order = order;
+        g.layout_row_ptr = nrp;
+        g.split_k = K;
+        g.split_mrows = mrows;
+        g.part_row0 = prow;
+        return true;
+    }
+    return false;
+}
+
 template <typename T>
 int upload(T **dst, const std::vector<T> &src) {
     const size_t bytes = std::max<size_t>(1, src.size()) * sizeof(T);
@@ -368,7 +446,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
     const char *want = std::getenv("QLDPC_VARIANT");
     const bool v1_only = want && std::strcmp(want, "v1") == 0;
-    if (v1_only || !plan_v2(*g, row_ptr)) plan(*g);
+    if (v1_only || (!plan_v2(*g, row_ptr) && !plan_v2_split(*g, row_ptr))) plan(*g);
     if (want && std::strcmp(want, "v2") == 0 && g->variant != VAR_V2)
         return fail(QLDPC_EUNSUP, "QLDPC_VARIANT=v2 but no V2 instantiation holds this graph");
     const int T = g->T, EPL = g->EPL;
@@ -390,7 +468,11 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     const bool reg = g->variant == VAR_REG_LDS || v2;
     const int G4 = v2 ? (g->v2R + g->v2RG) / 4 : (reg ? EPL_REG / 4 : (EPL + 3) / 4);
     const int TS = reg ? REG_TSTRIDE : T;
-    std::vector<uint32_t> meta((size_t)G4 * TS * 4, 0);
+    const int NPARTS = (T + TS - 1) / TS;  // V2 split: parts of TS lanes, each its own [G4][TS][4] block
+    auto midx = [&](int l, int k) -> size_t {
+        return ((size_t)((l / TS) * G4 + k / 4) * TS + (size_t)(l % TS)) * 4 + (size_t)(k % 4);
+    };
+    std::vector<uint32_t> meta((size_t)G4 * TS * 4 * NPARTS, 0);
     std::vector<int32_t> lrow0(T, v2 ? 0 : -1), lhead(T, 0), lnst(T, 0), lepl(T, EPL);
     // Lane l holds edges [e_begin, e_end) of its wave (v1: one "wave" of T lanes).
     // V2 metadata differs in three ways: the END of a lane's tail (a row begun
@@ -424,8 +506,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // (descending) so each term's bits are a prefix: stage[off[kk] + rank[b]].
     g->vn_k0 = g->dv_max;
     std::vector<int32_t> hd_bits, hd_dv, stage_off(std::max(1, g->dv_max), 0), rank(n, -1);
-    if (v2 && g->v2RG > 0 && g->dv_max > 4) {
-        g->vn_k0 = 4;
+    // (split frames: every term after the first goes through the stage)
+    if (v2 && ((g->v2RG > 0 && g->dv_max > 4) || (g->split_k > 1 && g->dv_max > 1))) {
+        g->vn_k0 = g->split_k > 1 ? 1 : 4;
         for (int i = 0; i < n; ++i)
             if (dv[i] > g->vn_k0) hd_bits.push_back(i);
         std::stable_sort(hd_bits.begin(), hd_bits.end(), [&](int x, int y) { return dv[x] > dv[y]; });
@@ -444,8 +527,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     const int S4 = G4 * 4;  // V2 slots per lane (register + scratch)
     auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm,
                           std::vector<uint32_t> &mt2, std::vector<uint64_t> &vex) -> int {
-        mt.assign((size_t)G4 * TS * 4, 0);
-        mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 : 0, 0);
+        mt.assign((size_t)G4 * TS * 4 * NPARTS, 0);
+        mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 * NPARTS : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
         vex.assign(v2 ? (size_t)W * g->dv_max * S4 : 0, 0);
         perm = ledge;
@@ -485,7 +568,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                             vex[((size_t)w * g->dv_max + kpos[ed]) * S4 + k] |= 1ull << li;
                         }
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
-                            mt2[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] =
+                            mt2[midx(l, k)] =
                                 (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
                         if (e == lrp[j]) {
                             wd |= META_START;
@@ -496,7 +579,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                             return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
                         prev_row = j;
                     }
-                    mt[((size_t)(k / 4) * TS + l) * 4 + (k % 4)] = wd;
+                    mt[midx(l, k)] = wd;
                 }
             }
         }
@@ -558,6 +641,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->slot_meta2, meta2)) || (rc = upload(&dg->slot_meta2_ms, meta2_ms)) ||
             (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
             (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
+            (rc = upload(&dg->part_row0, g->part_row0)) ||
             (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
@@ -588,6 +672,7 @@ int check_params(const qldpc_params *p) {
 
 // Per-workgroup scratch of the V2 kernels: overflow message slots, then the VN stage.
 long long v2_scratch_doubles(const qldpc_graph &g) {
+    if (g.split_k > 1) return 32;  // the stage is per frame (Workspace::gstage)
     return ((long long)g.v2RG * REG_TSTRIDE + g.stage_doubles + 31) / 32 * 32;
 }
 
@@ -610,6 +695,18 @@ int ensure_codes(qldpc_graph *g, Workspace *w, int batch, hipStream_t stream) {
     return QLDPC_OK;
 }
 
+// Split frames: after the stream is idle, fail loudly if a part group timed
+// out waiting for its members (the kernel never hangs on it; results are void).
+int split_check(qldpc_graph *g, DeviceGraph *dg, hipStream_t stream) {
+    if (g->variant != VAR_V2 || g->split_k <= 1) return QLDPC_OK;
+    Workspace *w = workspace(dg, stream);
+    if (!w->split_ctl) return QLDPC_OK;
+    int err = 0;
+    HIP_TRY(hipMemcpy(&err, w->split_ctl + 16, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) return fail(QLDPC_EHIP, "split frame: a part group failed to meet (results void)");
+    return QLDPC_OK;
+}
+
 // Enqueue the decoder for `batch` device-resident frames on `stream`.  For the
 // V2 kernel the frames' palette + codes are taken from the stream's workspace
 // when `codes_ready` (written by build_frames), else computed here from llr.
@@ -626,12 +723,15 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         std::lock_guard<std::mutex> lk(dg->mu);
         if (dg->occ[alg] == 0) {
             int b = 0;
-            if (v2) HIP_TRY(occupancy_v2(g->v2R, g->v2RG, alg, g->T, lds, &b));
+            if (v2) HIP_TRY(occupancy_v2(g->v2R, g->v2RG, g->split_k, alg, block_threads(*g), lds, &b));
             else HIP_TRY(occupancy(g->variant, alg, g->T, lds, &b));
             if (b <= 0) return fail(QLDPC_EUNSUP, "decoder kernel cannot be resident with this graph shape");
             dg->occ[alg] = b;
         }
         wgs = std::min(batch, dg->occ[alg] * dg->num_cus);
+        // split frames: every workgroup of the device (each XCD must hold whole
+        // part groups; the claim protocol needs >= split_k of them per XCD)
+        if (v2 && g->split_k > 1) wgs = dg->occ[alg] * dg->num_cus;
         w = workspace(dg, stream);
         if (!w->counter) HIP_TRY(hipMalloc(&w->counter, 64));
         if (v2) {
@@ -639,6 +739,18 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
                 return fail(QLDPC_EINVAL, "frame codes were not built for this batch");
             int rc = ensure_codes(g, w, batch, stream);
             if (rc) return rc;
+            if (g->split_k > 1 && (size_t)batch > w->split_frames) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                (void)hipFree(w->split_ctl);
+                (void)hipFree(w->gtotal);
+                (void)hipFree(w->gstage);
+                w->split_ctl = nullptr; w->gtotal = nullptr; w->gstage = nullptr; w->split_frames = 0;
+                const size_t slots = (size_t)batch + 64;
+                HIP_TRY(hipMalloc(&w->split_ctl, (32 + 3 * 16 * slots) * sizeof(int)));
+                HIP_TRY(hipMalloc(&w->gtotal, (size_t)batch * (g->n + 1) * sizeof(double)));
+                HIP_TRY(hipMalloc(&w->gstage, (size_t)batch * std::max<long long>(1, g->stage_doubles) * sizeof(double)));
+                w->split_frames = (size_t)batch;
+            }
         }
         {
             const long long per = v2 ? v2_scratch_doubles(*g)
@@ -656,7 +768,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         }
     }
     DecodeArgs a{};
-    a.n = g->n; a.m = g->m; a.E = g->E; a.T = g->T; a.EPL = g->EPL; a.dv_max = g->dv_max; a.max_dc = g->max_dc;
+    a.n = g->n; a.m = g->m; a.E = g->E; a.T = block_threads(*g); a.EPL = g->EPL; a.dv_max = g->dv_max; a.max_dc = g->max_dc;
     a.slot_meta = dg->slot_meta; a.lane_row0 = dg->lane_row0; a.lane_head = dg->lane_head;
     a.lane_nst = dg->lane_nst; a.lane_epl = dg->lane_epl;
     if (v2 && alg >= 2) a.slot_meta = dg->slot_meta_ms;
@@ -678,6 +790,22 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.row_orig = dg->row_orig;
+    a.split_k = v2 ? g->split_k : 1;
+    if (v2 && g->split_k > 1) {
+        const int slots = (int)w->split_frames + 64;
+        a.split_mrows = g->split_mrows;
+        a.split_slots = slots;
+        a.part_row0 = dg->part_row0;
+        a.split_claim = w->split_ctl;
+        a.split_err = w->split_ctl + 16;
+        a.split_pub = w->split_ctl + 32;
+        a.split_sync = a.split_pub + 16 * slots;
+        a.split_mis = a.split_sync + 16 * slots;
+        a.gtotal = w->gtotal;
+        a.gstage = w->gstage;
+        a.stage_frame_doubles = g->stage_doubles;
+        HIP_TRY(hipMemsetAsync(w->split_ctl, 0, (32 + 3 * 16 * (size_t)slots) * sizeof(int), stream));
+    }
     a.nc = (g->n + 3) / 4;
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
     a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
@@ -685,7 +813,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
 #ifdef QL_PHASE_STAMPS
-    const size_t nst = (size_t)wgs * (g->T / 64) * NUM_STAMPS;
+    const size_t nst = (size_t)wgs * (block_threads(*g) / 64) * NUM_STAMPS;
     uint64_t *d_st = nullptr;
     HIP_TRY(hipMalloc(&d_st, nst * sizeof(uint64_t)));
     HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
@@ -813,6 +941,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->hd_dv);
         (void)hipFree(d->stage_off);
         (void)hipFree(d->row_orig);
+        (void)hipFree(d->part_row0);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->vn_exec);
@@ -827,6 +956,9 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(kv.second.codes);
             (void)hipFree(kv.second.palette);
             (void)hipFree(kv.second.pal_ok);
+            (void)hipFree(kv.second.split_ctl);
+            (void)hipFree(kv.second.gtotal);
+            (void)hipFree(kv.second.gstage);
         }
         HostIO &io = d->io;
         (void)hipFree(io.llr); (void)hipFree(io.post); (void)hipFree(io.synd); (void)hipFree(io.bits); (void)hipFree(io.ok); (void)hipFree(io.iters);
@@ -855,13 +987,15 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
     if (lanes) *lanes = g->T;
     if (edges_per_lane) *edges_per_lane = g->EPL;
     if (lds_bytes) *lds_bytes = (int32_t)lds;
-    if (variant) *variant = (g->variant == VAR_V2 && g->v2RG > 0) ? "v2_hybrid" : variant_name(g->variant);
+    if (variant)
+        *variant = (g->variant == VAR_V2 && g->split_k > 1) ? "v2_split"
+                   : (g->variant == VAR_V2 && g->v2RG > 0) ? "v2_hybrid" : variant_name(g->variant);
     if (workgroups) {
         int prev = 0;
         HIP_TRY(hipGetDevice(&prev));
         HIP_TRY(hipSetDevice(dg->device));
         int b = 0;
-        hipError_t e = g->variant == VAR_V2 ? occupancy_v2(g->v2R, g->v2RG, algorithm, g->T, lds, &b)
+        hipError_t e = g->variant == VAR_V2 ? occupancy_v2(g->v2R, g->v2RG, g->split_k, algorithm, block_threads(*g), lds, &b)
                                             : occupancy(g->variant, algorithm, g->T, lds, &b);
         (void)hipSetDevice(prev);
         if (e != hipSuccess) return hip_fail(e, "occupancy");
@@ -940,7 +1074,7 @@ int qldpc_decode_batch(qldpc_graph *g, const qldpc_params *p, int32_t batch, con
                         HIP_TRY(hipMemcpyAsync(posterior_out + f0 * n, io.post, nb * n * sizeof(double),
                                                hipMemcpyDeviceToHost, io.stream));
                     HIP_TRY(hipStreamSynchronize(io.stream));
-                    return QLDPC_OK;
+                    return split_check(g, dg, io.stream);
                 };
                 r = fin();
             }

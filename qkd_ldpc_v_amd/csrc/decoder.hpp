@@ -96,6 +96,19 @@ struct DecodeArgs {
     const uint32_t *slot_meta2;     // like slot_meta: stage index of the slot's edge
     long long stage_wg_offset;      // doubles from a workgroup's scratch base to its stage
     const int32_t *row_orig;        // V2: layout row -> original row (syndrome index)
+    // V2 split frames (split_k > 1 workgroups of one XCD per frame)
+    int split_k;                    // parts per frame (1: not split)
+    int split_mrows;                // rows of the largest part (LDS rows array)
+    int split_slots;                // group slots per XCD in the arrays below
+    const int32_t *part_row0;       // [split_k + 1] first layout row of each part
+    int *split_claim;               // [16] per-XCD claim counters
+    int *split_pub;                 // [16][slots] frame + 1, published by rank 0
+    int *split_sync;                // [16][slots] group barrier arrivals
+    int *split_mis;                 // [16][slots] iteration + 1 of the last row mismatch
+    double *gtotal;                 // [batch][n + 1] the frames' totals
+    int *split_err;                 // set when a part group failed to meet (results void)
+    double *gstage;                 // [batch][stage_frame_doubles] split frames' VN stage
+    long long stage_frame_doubles;
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -113,9 +126,9 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
                                hipStream_t stream);
 
-size_t lds_bytes_v2(int alg, int n, int m, int T);
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false);
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
-hipError_t occupancy_v2(int R, int RG, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
+hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
                             uint8_t *pal_ok, hipStream_t stream);
 size_t trials_lds_bytes(int n);

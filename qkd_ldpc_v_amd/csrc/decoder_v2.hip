@@ -37,13 +37,16 @@ constexpr int V2_PAL_OFF = V2_CTRL;                    // 4 doubles
 constexpr int V2_CODES_OFF = V2_PAL_OFF + 32;          // one palette index byte per bit
 constexpr int V2_TOTAL_OFF = V2_CODES_OFF + V2_CODES_CAP;
 static_assert(V2_TOTAL_OFF % 16 == 0 && V2_TOTAL_OFF < 65536, "ds offset immediates are 16-bit");
+// Split frames (several workgroups per frame): the totals live in global
+// memory and the palette indices are read from the 2-bit global codes; LDS
+// holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
     size_t total, rows, rowflag, tail, tailneg, codes, palette, bytes;
-    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum) {
+    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false) {
         palette = V2_PAL_OFF;
-        codes = V2_CODES_OFF;
-        size_t o = V2_TOTAL_OFF;
-        total = o; o = al16(o + (size_t)(n + 1) * 8);
+        codes = split ? 0 : V2_CODES_OFF;
+        size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
+        total = o; o = split ? o : al16(o + (size_t)(n + 1) * 8);
         rows = o; o = al16(o + (size_t)m * (minsum ? 16 : 8));  // SPA: product; min-sum: {min1, min2}
         rowflag = o; o = al16(o + (minsum ? (size_t)m : 0));
         tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
@@ -61,7 +64,39 @@ constexpr int v2_max_threads() { return v2_threads_for(R); }
 template <int S>
 constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 
-template <int ALG, int R, int RG>
+// SPLIT: a frame is decoded by a.split_k workgroups of one XCD (planner
+// parts: contiguous blocks of 16 waves' rows), which meet at every phase
+// boundary through a global arrival counter; totals are in global memory.
+template <bool SPLIT>
+__device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
+    if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true);
+    else return V2Layout(a.n, a.m, a.nc, a.T, minsum);
+}
+
+constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
+
+// Barrier of a split frame's part group: every wave's global stores reach L2
+// (the group shares this XCD's L2), one arrival per workgroup, a bounded wait
+// for the group's count, then the frame's totals are re-read past L1.
+__device__ __forceinline__ void group_sync(int *ctr, int target, int *err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (++spins >= V2_SPLIT_SPIN_LIMIT) {  // reported; the frame's results are void
+                atomicOr(err, 1);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    asm volatile("buffer_inv sc1" ::: "memory");
+}
+
+template <int ALG, int R, int RG, bool SPLIT>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
@@ -69,7 +104,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     constexpr bool NORM = (ALG == 2 || ALG == 4);
     constexpr int S = R + RG;
     static_assert(S <= 64, "VN phase masks are 64-bit");
-    constexpr bool GATHER = RG > 0;  // sparse VN terms through the stage (hybrid shape)
+    // VN terms kk >= vn_k0 through a global stage written by the message pass
+    // and summed per bit in one gather pass: the hybrid shape's sparse
+    // high-degree terms, and on split frames every term after the first (the
+    // totals are global there anyway; the gather reads the stage coalesced).
+    constexpr bool GATHER = RG > 0 || SPLIT;
     constexpr int KT = v2_tail_slots<S>();
 
     const int tid = threadIdx.x;
@@ -77,14 +116,18 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // threshold_matrix disabled == clipping at +inf (|v| > inf never holds; NaN passes)
     const double thr = a.thr_on ? a.thr : __builtin_inf();
     const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
-    const V2Layout L(n, m, nc, T, !SPA_FAM);
+    const V2Layout L = v2_layout<SPLIT>(a, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
+    int *s_part = reinterpret_cast<int *>(smem) + 2;  // SPLIT: rank, sync slot
     double *total = reinterpret_cast<double *>(smem + V2_TOTAL_OFF);
-    double *rowA = reinterpret_cast<double *>(smem + L.rows);   // SPA
-    double2 *rowAB = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
+    double *const rowA_lds = reinterpret_cast<double *>(smem + L.rows);    // SPA
+    double2 *const rowAB_lds = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
+    uint8_t *const rowflag_lds = smem + L.rowflag;  // min-sum: bit0 syndrome, bit1 row mismatch, bit2 negative parity
+    double *rowA = rowA_lds;
+    double2 *rowAB = rowAB_lds;
+    uint8_t *rowflag = rowflag_lds;
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
-    uint8_t *rowflag = smem + L.rowflag;  // min-sum: bit0 syndrome, bit1 row mismatch, bit2 negative parity
     double2 *tailagg = reinterpret_cast<double2 *>(smem + L.tail);
     int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
     uint8_t *codes = smem + V2_CODES_OFF;
@@ -102,19 +145,25 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // (constant address space: read-only for the kernel's lifetime, so the loads are s_load)
     typedef const __attribute__((address_space(4))) uint64_t const_u64;
     const const_u64 *vn_exec = (const const_u64 *)(a.vn_exec + (size_t)wave * a.dv_max * S);
+    // SPLIT: this workgroup's XCD (groups never span two L2s)
+    uint32_t xcc = 0;
+    if constexpr (SPLIT) {
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        xcc &= 15u;
+    }
     double *stage = a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.stage_wg_offset;
-    // (only used by the GATHER instantiations)
-    const __amdgpu_buffer_rsrc_t stage_rs =
+    // (only used by the GATHER instantiations; split frames re-point both per frame)
+    __amdgpu_buffer_rsrc_t stage_rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, GATHER ? 0x7fffffff : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
+    __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.slot_meta2, (short)0, GATHER ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
     const int k0 = GATHER ? a.vn_k0 : a.dv_max;
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
-    const int head_in = a.lane_head[tid];
-    const int row0_in = a.lane_row0[tid];
-    const int nst = a.lane_nst[tid];
-    const int epl = __builtin_amdgcn_readfirstlane(a.lane_epl[tid]);
+    const int head_in0 = a.lane_head[tid];
+    const int row0_in0 = a.lane_row0[tid];
+    const int nst0 = a.lane_nst[tid];
+    const int epl0 = __builtin_amdgcn_readfirstlane(a.lane_epl[tid]);
     const int lane = tid & 63;
     const int up = (lane == 0) ? 0 : lane - 1;
     int epoch = 0;
@@ -126,12 +175,84 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 #endif
 
     for (;;) {
-        if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        if constexpr (SPLIT) {
+            // Claim (slot, rank) on this XCD's counter; rank 0 of a slot draws
+            // the frame and publishes it to the slot's other ranks.
+            if (tid == 0) {
+                const int t = atomicAdd(a.split_claim + xcc, 1);
+                const int slot = t / a.split_k, rank = t % a.split_k;
+                const int si = (int)xcc * a.split_slots + slot;
+                int f = a.batch;
+                if (slot < a.split_slots) {
+                    int *pub = a.split_pub + si;
+                    if (rank == 0) {
+                        f = atomicAdd(a.frame_counter, 1);
+                        __hip_atomic_store(pub, f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        int v, spins = 0;
+                        while ((v = __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 &&
+                               ++spins < V2_SPLIT_SPIN_LIMIT)
+                            __builtin_amdgcn_s_sleep(2);
+                        // a group that never forms (cannot happen with >= split_k
+                        // workgroups per XCD) is reported, never waited on forever
+                        if (v == 0) atomicOr(a.split_err, 1);
+                        f = v ? v - 1 : a.batch;
+                    }
+                }
+                *s_frame = f;
+                s_part[0] = rank;
+                s_part[1] = si;
+            }
+        } else {
+            if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        }
         STAMP(ST_SETUP);
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
         const int f = *s_frame;
         if (f >= a.batch) break;
+        // SPLIT: this part's lanes, waves, metadata and rows; the group barrier
+        const int rank = SPLIT ? __builtin_amdgcn_readfirstlane(s_part[0]) : 0;
+        const int tg = SPLIT ? rank * REG_TSTRIDE + tid : tid;
+        const int head_in = SPLIT ? a.lane_head[tg] : head_in0;
+        const int row0_in = SPLIT ? a.lane_row0[tg] : row0_in0;
+        const int nst = SPLIT ? a.lane_nst[tg] : nst0;
+        const int epl = SPLIT ? __builtin_amdgcn_readfirstlane(a.lane_epl[tg]) : epl0;
+        int gsync_n = 0;
+        int *gsync = nullptr, *gmis = nullptr;
+        if constexpr (SPLIT) {
+            const int si = __builtin_amdgcn_readfirstlane(s_part[1]);
+            gsync = a.split_sync + si;
+            gmis = a.split_mis + si;
+            meta.init(a.slot_meta + (size_t)rank * (S / 4) * REG_TSTRIDE * 4, tid, T);
+            const int wg = rank * (REG_TSTRIDE / 64) + wave;
+            vn_mask = a.vn_mask + (size_t)wg * a.dv_max;
+            vn_exec = (const const_u64 *)(a.vn_exec + (size_t)wg * a.dv_max * S);
+            const int rb = a.part_row0[rank];
+            rowA = rowA_lds - rb;
+            rowAB = rowAB_lds - rb;
+            rowflag = rowflag_lds - rb;
+            total = a.gtotal + (size_t)f * (n + 1);
+            stage = a.gstage + (size_t)f * a.stage_frame_doubles;
+            stage_rs = __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, 0x7fffffff, 0x00020000);
+            meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(a.slot_meta2 + (size_t)rank * (S / 4) * REG_TSTRIDE * 4), (short)0,
+                S / 4 * REG_TSTRIDE * 16, 0x00020000);
+        }
+        // Phase boundary: the workgroup barrier, or for SPLIT the group's: every
+        // wave's global stores reach L2 (the group shares this XCD's L2), one
+        // arrival per workgroup, then the frame's totals are re-read past L1.
+#define psync()                                                              \
+    do {                                                                     \
+        if constexpr (SPLIT) {                                               \
+            gsync_n += a.split_k;                                            \
+            group_sync(gsync, gsync_n, a.split_err);                         \
+        } else {                                                             \
+            __syncthreads();                                                 \
+        }                                                                    \
+    } while (0)
+        const int bit_lo = SPLIT ? (int)((long long)n * rank / a.split_k) : 0;
+        const int bit_hi = SPLIT ? (int)((long long)n * (rank + 1) / a.split_k) : n;
         const uint8_t *sy = a.synd + (size_t)f * m;
         // Target syndrome bits of the rows this lane starts (bit i = i-th START),
         // and of the row it finishes for the lane before (split row).
@@ -148,7 +269,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // flat load.
         const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.llr + (size_t)f * n), (short)0, paletted ? 0 : n * 8, 0x00020000);
-        {
+        const uint8_t *gcodes = a.codes + (size_t)f * nc;
+        if constexpr (SPLIT) {
+            if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
+        } else {
             // 2-bit codes -> one byte per bit (the message pass's llr lookup is
             // then a byte read, no shift/mask arithmetic)
             const uint8_t *cs = a.codes + (size_t)f * nc;
@@ -163,15 +287,19 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
         auto llr_of = [&](int col) -> double {
-            if (paletted) return pal[codes[col]];
+            if constexpr (SPLIT) {
+                if (paletted) return pal[(gcodes[col >> 2] >> ((col & 3) * 2)) & 3];
+            } else {
+                if (paletted) return pal[codes[col]];
+            }
             return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
         };
         // total starts as the channel LLRs: the check-node scan of iteration 0
         // reads the channel decision from it, and bits of degree 0 keep it.
-        for (int i = tid; i < n; i += T) total[i] = llr_of(i);
-        if (tid == 0) total[n] = 1.0;  // dummy column
+        for (int i = bit_lo + tid; i < bit_hi; i += T) total[i] = llr_of(i);
+        if (tid == 0 && rank == 0) total[n] = 1.0;  // dummy column
         STAMP(ST_SETUP);
-        __syncthreads();
+        psync();
         STAMP(ST_SETUP_WAIT);
 
         int iters = a.max_it, okv = 0;
@@ -296,11 +424,16 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     }
                 }
             }
-            if (mis) *s_flag = epoch;
+            if constexpr (SPLIT) {
+                if (mis) __hip_atomic_store(gmis, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (mis) *s_flag = epoch;
+            }
             STAMP(ST_CN1);
-            __syncthreads();
+            psync();
             STAMP(ST_CN1_WAIT);
-            const bool anymis = *s_flag == epoch;
+            const bool anymis = SPLIT ? (__hip_atomic_load(gmis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it + 1)
+                                      : (*s_flag == epoch);
             // SPA: rp / t by div_rn_safe when every t of this wave came out of
             // tanh's common path (|t| in [2^-55, 1]) and every row product of the
             // wave is at least 2^-900 in magnitude: the operand range where the
@@ -366,7 +499,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
             }
             STAMP(ST_CN3);
-            __syncthreads();
+            psync();
             STAMP(ST_VN0_WAIT);
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
             for (int kk = 1; kk < k0; ++kk) {
@@ -388,21 +521,42 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                             total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
                 });
                 STAMP(ST_VNK);
-                __syncthreads();
+                psync();
                 STAMP(ST_VNK_WAIT);
             }
             if constexpr (GATHER) {
                 // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
                 if (k0 < a.dv_max) {
-                    for (int i = tid; i < a.n_hd; i += T) {
-                        const int b = a.hd_bits[i];
-                        const int dvb = a.hd_dv[i];
-                        double sacc = total[b];
-                        for (int kk = k0; kk < dvb; ++kk) sacc = sacc + stage[a.stage_off[kk] + i];
-                        total[b] = sacc;
+                    // (split frames: each part sums its share of the bits)
+                    const int h0 = SPLIT ? (int)((long long)a.n_hd * rank / a.split_k) : 0;
+                    const int h1 = SPLIT ? (int)((long long)a.n_hd * (rank + 1) / a.split_k) : a.n_hd;
+                    // four bits per lane at a time: their stage loads overlap
+                    for (int i0 = h0 + tid; i0 < h1; i0 += 4 * T) {
+                        int b[4], dvb[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int i = i0 + j * T;
+                            b[j] = (i < h1) ? a.hd_bits[i] : -1;
+                            dvb[j] = (i < h1) ? a.hd_dv[i] : 0;
+                        }
+                        double sacc[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) sacc[j] = (b[j] >= 0) ? total[b[j]] : 0.0;
+                        for (int kk = k0; kk < a.dv_max; ++kk) {
+                            const int off = a.stage_off[kk];
+                            double v[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = (kk < dvb[j]) ? stage[off + i0 + j * T] : 0.0;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (kk < dvb[j]) sacc[j] = sacc[j] + v[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (b[j] >= 0) total[b[j]] = sacc[j];
                     }
                     STAMP(ST_VNK);
-                    __syncthreads();
+                    psync();
                     STAMP(ST_VNK_WAIT);
                 }
             }
@@ -415,12 +569,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const bool zero_post = ADAPT && !had_vn;
         uint8_t *bits = a.bits + (size_t)f * n;
         double *post = a.post ? a.post + (size_t)f * n : nullptr;
-        for (int i = tid; i < n; i += T) {
+        for (int i = bit_lo + tid; i < bit_hi; i += T) {
             const double z = total[i];
             bits[i] = (z <= 0.0) ? 1 : 0;
             if (post) post[i] = zero_post ? 0.0 : z;
         }
-        if (tid == 0) {
+        if (tid == 0 && rank == 0) {
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
         }
@@ -435,6 +589,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     }
 #endif
 }
+#undef psync
 
 // Palette + 2-bit codes of each frame's LLRs (one workgroup per frame).  Wave 0
 // collects up to 4 distinct values (bitwise) in first-occurrence order; a frame
@@ -491,19 +646,20 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
 
 using KernelFn = void (*)(DecodeArgs);
 
-template <int R, int RG>
+template <int R, int RG, bool SPLIT = false>
 KernelFn pick_v2(int alg) {
     switch (alg) {
-    case 0: return decode_v2_kernel<0, R, RG>;
-    case 1: return decode_v2_kernel<1, R, RG>;
-    case 2: return decode_v2_kernel<2, R, RG>;
-    case 3: return decode_v2_kernel<3, R, RG>;
-    case 4: return decode_v2_kernel<4, R, RG>;
-    default: return decode_v2_kernel<5, R, RG>;
+    case 0: return decode_v2_kernel<0, R, RG, SPLIT>;
+    case 1: return decode_v2_kernel<1, R, RG, SPLIT>;
+    case 2: return decode_v2_kernel<2, R, RG, SPLIT>;
+    case 3: return decode_v2_kernel<3, R, RG, SPLIT>;
+    case 4: return decode_v2_kernel<4, R, RG, SPLIT>;
+    default: return decode_v2_kernel<5, R, RG, SPLIT>;
     }
 }
 
-KernelFn kernel_v2(int R, int RG, int alg) {
+KernelFn kernel_v2(int R, int RG, int split_k, int alg) {
+    if (split_k > 1) return pick_v2<V2_R_TIGHT, 0, true>(alg);
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
     if (R == V2_R_TIGHT) return pick_v2<V2_R_TIGHT, 0>(alg);
     if (R == V2_R_SMALL) return pick_v2<V2_R_SMALL, 0>(alg);
@@ -512,12 +668,12 @@ KernelFn kernel_v2(int R, int RG, int alg) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T) {
-    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2).bytes;
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split) {
+    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, split).bytes;
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
-    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.alg);
+    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
@@ -525,8 +681,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     return hipGetLastError();
 }
 
-hipError_t occupancy_v2(int R, int RG, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
-    KernelFn k = kernel_v2(R, RG, alg);
+hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
+    KernelFn k = kernel_v2(R, RG, split_k, alg);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;

@@ -192,8 +192,27 @@ def test_c5_irregular_v1_global_message_variant(gpu_available, alg, prim, sec):
 
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.AOMSA, 0.55, 1.2)])
 def test_c4_100k_all_global_variant(gpu_available, alg, prim, sec):
-    assert graph("c4s_n102400_m32001.alist").plan(0, alg)["variant"] == "glb_glb"
-    assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=0.038, batch=3, max_it=6, seed=4)
+    assert graph("c4s_n102400_m32001.alist", "v1").plan(0, alg)["variant"] == "glb_glb"
+    assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=0.038, batch=3, max_it=6, seed=4, variant="v1")
+
+
+# n = 100k: a frame is split over 8 workgroups of one XCD (capi.hip plan_v2_split)
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_c4_100k_split_variant(gpu_available, alg, prim, sec):
+    assert graph("c4s_n102400_m32001.alist").plan(0, alg)["variant"] == "v2_split"
+    assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=0.038, batch=10, max_it=8, seed=40 + alg)
+
+
+def test_c4_100k_split_full_decode(gpu_available):
+    # 50 iterations: converging frames exit early, the rest run to the cap
+    out, oi = assert_parity("c4s_n102400_m32001.alist", Q.SPA, 0, 0, qber=0.038, batch=6, max_it=50, seed=9)
+    assert out.iterations.min() < 50
+
+
+@pytest.mark.parametrize("batch", [1, 2])
+def test_c4_100k_split_few_frames(gpu_available, batch):
+    # fewer frames than XCDs: most part groups draw no frame and leave
+    assert_parity("c4s_n102400_m32001.alist", Q.OMSA, 0.77, 0, qber=0.038, batch=batch, max_it=5, seed=70 + batch)
 
 
 @pytest.mark.parametrize("max_it", [1, 2, 3])
