@@ -4,7 +4,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := qkd_ldpc_v_amd
 CSRC := $(PKG)/csrc
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result
+HIPFLAGS := --offload-arch=$(ARCH) $(EXTRA_HIPFLAGS) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result
 LIB := $(PKG)/libqkdldpc_hip.so
 ORACLE := oracle/libqkdldpc_oracle.so
 HOSTCHK := $(PKG)/host/host_mirror_check
@@ -58,3 +58,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean stamps valu_bench
+
+# A/B experiment build: `make ab AB=name AB_FLAGS=-D...` -> qkd_ldpc_v_amd/ab/name/
+# (selected at run time with QLDPC_AB_BUILD=name; never the product)
+AB ?= x
+ab:
+	mkdir -p $(PKG)/ab/$(AB)
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/decoder_v2.hip -o $(PKG)/ab/$(AB)/decoder_v2.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/capi.o $(CSRC)/loaders.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
+.PHONY: ab

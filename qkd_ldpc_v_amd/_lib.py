@@ -17,6 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqkdldpc_hip.so")
 if os.environ.get("QLDPC_DIAG_STAMPS") == "1":  # diagnostic phase-stamp build (Makefile target `stamps`)
     LIB_PATH = os.path.join(_HERE, "diag", "libqkdldpc_hip.so")
+if os.environ.get("QLDPC_AB_BUILD"):  # A/B experiments: an alternative in-tree build, qkd_ldpc_v_amd/ab/<name>/
+    LIB_PATH = os.path.join(_HERE, "ab", os.environ["QLDPC_AB_BUILD"], "libqkdldpc_hip.so")
 
 QLDPC_OK = 0
 ERROR_NAMES = {-1: "EINVAL", -2: "EHIP", -3: "EIO", -4: "ENOMEM", -5: "EUNSUP"}

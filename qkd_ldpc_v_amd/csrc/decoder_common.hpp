@@ -171,6 +171,23 @@ struct MetaSrc {
         }
     }
 };
+// Issue priority of a SIMD's waves, rotated slot group by slot group: the
+// sequencer otherwise favours the oldest wave, so a SIMD's four waves finish a
+// phase one after another and the last runs alone (one wave cannot issue
+// dependent FP64 back to back).  Rotating the favoured wave keeps them level.
+// A SIMD holds waves w, w + 4, w + 8, w + 12 of a workgroup, told apart by
+// w >> 2; the rotation runs backwards through them (measured: C2 SPA -5.6%,
+// C3 OMSA -3%, tools/ab_bench.sh).
+__device__ __forceinline__ void rotate_prio(int g) {
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
+    switch ((3 * g + wv) & 3) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 // Same, but only the slots a wave actually holds: `epl_s` is wave-uniform (an
 // SGPR), so each slot costs a scalar compare-and-branch, no VALU.  Slots past
 // a lane's last row are dummies, but a lane whose last row continues into the
@@ -184,6 +201,7 @@ struct MetaSrcW : MetaSrc<R> {
         asm volatile("" : "+s"(epl_s));
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
+            rotate_prio(g);
             if (4 * g < epl_s) {
                 const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
                 f(4 * g + 0, (uint32_t)q[0]);
@@ -200,6 +218,9 @@ struct MetaSrcW : MetaSrc<R> {
         asm volatile("" : "+s"(epl_s));
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
+#ifdef QL_PRIO_MORE
+            rotate_prio(g);
+#endif
             if (4 * g < epl_s) {
                 const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
                 const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rs2, this->voff, g * REG_TSTRIDE * 16, 0);
@@ -216,6 +237,9 @@ struct MetaSrcW : MetaSrc<R> {
     __device__ __forceinline__ void each_group_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
+#ifdef QL_PRIO_MORE
+            rotate_prio(g);
+#endif
             const uint32_t w = (4 * g < 32) ? mlo : mhi;
             const uint32_t bits = (w >> ((4 * g) & 31)) & 15u;
             if (bits) {
