@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
                 if (4 * j + s < n && bo[4 * j + s]) byte |= 1 << (2 * s);
             cs[j] = (uint8_t)byte;
         }
-        if (threadIdx.x < 4) palette[f * 4 + threadIdx.x] = threadIdx.x == 0 ? lp : (threadIdx.x == 1 ? -lp : 0.0);
+        if (threadIdx.x < 4) palette[f * 4 + threadIdx.x] = threadIdx.x == 1 ? -lp : lp;  // unused 2, 3 repeat entry 0
         if (threadIdx.x == 0) pal_ok[f] = 1;
     }
     uint8_t *s = synd + f * (size_t)m;

@@ -37,11 +37,15 @@ constexpr int V2_PAL_OFF = V2_CTRL;                    // 4 doubles
 constexpr int V2_CODES_OFF = V2_PAL_OFF + 32;          // one palette index byte per bit
 constexpr int V2_TOTAL_OFF = V2_CODES_OFF + V2_CODES_CAP;
 static_assert(V2_TOTAL_OFF % 16 == 0 && V2_TOTAL_OFF < 65536, "ds offset immediates are 16-bit");
+// SPA iteration 0 on frames whose channel LLRs are all +-L: entry 0 is
+// t0 = tanh(L / 2.), entry d >= 1 the clipped 2 * atanh(|rp| / t0) of a row of
+// degree d (rows have <= 32 edges: plan_v2).
+constexpr int V2_A0_ENTRIES = 64;
 // Split frames (several workgroups per frame): the totals live in global
 // memory and the palette indices are read from the 2-bit global codes; LDS
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
-    size_t total, rows, rowflag, tail, tailneg, codes, palette, bytes;
+    size_t total, rows, rowflag, tail, tailneg, a0tab, codes, palette, bytes;
     __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
@@ -51,6 +55,7 @@ struct V2Layout {
         rowflag = o; o = al16(o + (minsum ? (size_t)m : 0));
         tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
         tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
+        a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
         bytes = o;
     }
 };
@@ -298,6 +303,28 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // reads the channel decision from it, and bits of degree 0 keep it.
         for (int i = bit_lo + tid; i < bit_hi; i += T) total[i] = llr_of(i);
         if (tid == 0 && rank == 0) total[n] = 1.0;  // dummy column
+        // SPA, iteration 0, every channel LLR +-L (the QKD_LDPC frame,
+        // src/qkd_ldpc_algorithm.cpp:1043-1052; unused palette entries repeat
+        // entry 0): b2c = +-L, so t = +-t0 with t0 = tanh(L / 2.) (tanh is odd
+        // in glibc), a row's running product of degree d is +-P_d with P_1 = t0,
+        // P_{j+1} = P_j * t0 (the sign of a product never changes its rounding),
+        // and every rp / t_k of the row is +-(P_d / t0).  So the iteration's
+        // messages are +-A[d], A[d] = clip(2 * atanh(P_d / t0)), computed once
+        // per frame by the same functions the general pass calls.
+        bool fast0 = false;
+        double *const a0tab = reinterpret_cast<double *>(smem + L.a0tab);
+        if constexpr (ALG == 0) {
+            const double L0 = __builtin_fabs(pal[0]);
+            fast0 = paletted && a.max_it > 0 && L0 >= 0x1p-20 && L0 <= 0x1p10 && __builtin_fabs(pal[1]) == L0 &&
+                    __builtin_fabs(pal[2]) == L0 && __builtin_fabs(pal[3]) == L0;
+            if (fast0 && tid < V2_A0_ENTRIES) {
+                int unused = 0;
+                const double t0 = ql_exact::tanh_half_clip(L0, 44.0, 1.0, &unused);
+                double P = t0;
+                for (int j = 1; j < tid; ++j) P = P * t0;
+                a0tab[tid] = (tid == 0) ? t0 : ql_exact::atanh2_clip(P / t0, thr, a.spa_ctop);
+            }
+        }
         STAMP(ST_SETUP);
         psync();
         STAMP(ST_SETUP_WAIT);
@@ -308,7 +335,141 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 #pragma unroll
             for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
         }
-        for (int it = 0;; ++it) {
+        // Message emission shared by both message passes: c2b, VN phase 0
+        // (total = llr + first message) and the hybrid/split VN stage.
+        auto emit = [&](int k, uint32_t mt, uint32_t mt2, double c) {
+            c2b.set(k, c);
+            const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
+            if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
+                const int col = (int)(mt & META_COL_MASK);
+                total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
+            }
+            if constexpr (GATHER) {
+                if (kp >= (uint32_t)k0 && kp != 63u) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, c), stage_rs, (int)(mt2 * 8),
+                                                          0, 0);
+                }
+            }
+        };
+        // VN phases 1 .. k0-1 and the staged terms (shared by iteration 0's fast path).
+        auto vn_phases = [&]() {
+            STAMP(ST_CN3);
+            psync();
+            STAMP(ST_VN0_WAIT);
+            // ---- remaining VN phases: the k-th message of every bit, in check order ----
+            for (int kk = 1; kk < k0; ++kk) {
+                const uint64_t vm = vn_mask[kk];
+                const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
+                const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
+                const const_u64 *ex = vn_exec + (size_t)kk * S;
+                // Four slots at a time: the four totals are read together (every
+                // lane; a bit's kk-th edge is unique, so no two lanes of the
+                // phase write one column), then added and written back by the
+                // lanes whose edge there is a kk-th one.
+                meta.each_group_masked(mlo, mhi, [&](int g, auto q, uint32_t) {
+                    double tv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
+                            total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
+                });
+                STAMP(ST_VNK);
+                psync();
+                STAMP(ST_VNK_WAIT);
+            }
+            if constexpr (GATHER) {
+                // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
+                if (k0 < a.dv_max) {
+                    // (split frames: each part sums its share of the bits)
+                    const int h0 = SPLIT ? (int)((long long)a.n_hd * rank / a.split_k) : 0;
+                    const int h1 = SPLIT ? (int)((long long)a.n_hd * (rank + 1) / a.split_k) : a.n_hd;
+                    // four bits per lane at a time: their stage loads overlap
+                    for (int i0 = h0 + tid; i0 < h1; i0 += 4 * T) {
+                        int b[4], dvb[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int i = i0 + j * T;
+                            b[j] = (i < h1) ? a.hd_bits[i] : -1;
+                            dvb[j] = (i < h1) ? a.hd_dv[i] : 0;
+                        }
+                        double sacc[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) sacc[j] = (b[j] >= 0) ? total[b[j]] : 0.0;
+                        for (int kk = k0; kk < a.dv_max; ++kk) {
+                            const int off = a.stage_off[kk];
+                            double v[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) v[j] = (kk < dvb[j]) ? stage[off + i0 + j * T] : 0.0;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                if (kk < dvb[j]) sacc[j] = sacc[j] + v[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (b[j] >= 0) total[b[j]] = sacc[j];
+                    }
+                    STAMP(ST_VNK);
+                    psync();
+                    STAMP(ST_VNK_WAIT);
+                }
+            }
+        };
+        int it0 = 0;
+        if (ALG == 0 && fast0) {
+            int head = head_in, row0 = row0_in;
+            uint32_t sm = smask_f;
+            asm volatile("" : "+v"(head), "+v"(row0), "+v"(sm));
+            // ---- SPA iteration 0 on a +-L frame (see fast0): t = +-t0, and
+            // per row its degree and sign (s xor parity of the negative
+            // LLRs = parity of the channel decisions) instead of a product
+            int2 *const rowI = reinterpret_cast<int2 *>(rowA);
+            const double t0 = a0tab[0];
+            int r = row0, par = 0, cnt = 0, cur_s = 0;
+            uint32_t zt = 0;
+            meta.each_upto(epl, [&](int k, uint32_t mt) {
+                const int col = (int)(mt & META_COL_MASK);
+                const double tv = total[col];
+                const int zb = (tv <= 0.0) ? 1 : 0;
+                if (k < KT) zt |= (uint32_t)zb << k;
+                const bool start = (mt & META_START) != 0;
+                c2b.set(k, __builtin_copysign(t0, tv));
+                cur_s = start ? (int)(sm & 1u) : cur_s;
+                sm = start ? (sm >> 1) : sm;
+                par = (start ? 0 : par) ^ zb;
+                cnt = (start ? 0 : cnt) + 1;
+                if (k > 0) r += start ? 1 : 0;
+                if (mt & META_END) rowI[r] = make_int2(cnt, par ^ cur_s);
+            });
+            {  // a row split across two lanes of this wave
+                const int ppar = __shfl(par, up, 64);
+                const int pcnt = __shfl(cnt, up, 64);
+                const int hpar = __builtin_popcount(zt & ((1u << head) - 1u)) & 1;
+                if (head > 0) rowI[row0] = make_int2(pcnt + head, ppar ^ hpar ^ s_row0);
+            }
+            STAMP(ST_CN1);
+            psync();
+            STAMP(ST_CN1_WAIT);
+            r = row0;
+            auto message0 = [&](int k, uint32_t mt, uint32_t mt2) {
+                if (k > 0) r += (mt & META_START) ? 1 : 0;
+                const int2 ri = rowI[r];
+                const double av = a0tab[ri.x & (V2_A0_ENTRIES - 1)];
+                const uint32_t neg = ((uint32_t)ri.y ^ (ql_exact::hi_word(c2b.get(k)) >> 31)) & 1u;
+                emit(k, mt, mt2, neg ? -av : av);  // sign of rp / t_k (:66-68)
+            };
+            if constexpr (GATHER) {
+                meta.each_upto2(epl, meta2_rs, message0);
+            } else {
+                meta.each_upto(epl, [&](int k, uint32_t mt) { message0(k, mt, 0u); });
+            }
+            vn_phases();
+            had_vn = true;
+            it0 = 1;
+        }
+        for (int it = it0;; ++it) {
             // SPA: iteration 0's b2c is the unclipped channel LLR (:21-29)
             const double lim_it = had_vn ? lim : 44.0;
             const double tlim_it = had_vn ? a.spa_tlim : 1.0;  // tanh(22) = 1
@@ -479,87 +640,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     }
                 }
                 if constexpr (ALG != 0) c = clip_msg(c, thr);  // (:73-74)
-                c2b.set(k, c);
-                const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-                if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
-                    const int col = (int)(mt & META_COL_MASK);
-                    total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
-                }
-                if constexpr (GATHER) {
-                    if (kp >= (uint32_t)k0 && kp != 63u) {
-                        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, c), stage_rs, (int)(mt2 * 8),
-                                                              0, 0);
-                    }
-                }
+                emit(k, mt, mt2, c);
             };
             if constexpr (GATHER) {
                 meta.each_upto2(epl, meta2_rs, message);
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
             }
-            STAMP(ST_CN3);
-            psync();
-            STAMP(ST_VN0_WAIT);
-            // ---- remaining VN phases: the k-th message of every bit, in check order ----
-            for (int kk = 1; kk < k0; ++kk) {
-                const uint64_t vm = vn_mask[kk];
-                const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
-                const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
-                const const_u64 *ex = vn_exec + (size_t)kk * S;
-                // Four slots at a time: the four totals are read together (every
-                // lane; a bit's kk-th edge is unique, so no two lanes of the
-                // phase write one column), then added and written back by the
-                // lanes whose edge there is a kk-th one.
-                meta.each_group_masked(mlo, mhi, [&](int g, auto q, uint32_t) {
-                    double tv[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
-                            total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
-                });
-                STAMP(ST_VNK);
-                psync();
-                STAMP(ST_VNK_WAIT);
-            }
-            if constexpr (GATHER) {
-                // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
-                if (k0 < a.dv_max) {
-                    // (split frames: each part sums its share of the bits)
-                    const int h0 = SPLIT ? (int)((long long)a.n_hd * rank / a.split_k) : 0;
-                    const int h1 = SPLIT ? (int)((long long)a.n_hd * (rank + 1) / a.split_k) : a.n_hd;
-                    // four bits per lane at a time: their stage loads overlap
-                    for (int i0 = h0 + tid; i0 < h1; i0 += 4 * T) {
-                        int b[4], dvb[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int i = i0 + j * T;
-                            b[j] = (i < h1) ? a.hd_bits[i] : -1;
-                            dvb[j] = (i < h1) ? a.hd_dv[i] : 0;
-                        }
-                        double sacc[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) sacc[j] = (b[j] >= 0) ? total[b[j]] : 0.0;
-                        for (int kk = k0; kk < a.dv_max; ++kk) {
-                            const int off = a.stage_off[kk];
-                            double v[4];
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) v[j] = (kk < dvb[j]) ? stage[off + i0 + j * T] : 0.0;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                if (kk < dvb[j]) sacc[j] = sacc[j] + v[j];
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (b[j] >= 0) total[b[j]] = sacc[j];
-                    }
-                    STAMP(ST_VNK);
-                    psync();
-                    STAMP(ST_VNK_WAIT);
-                }
-            }
+            vn_phases();
             had_vn = true;
         }
 
@@ -593,7 +681,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
 // Palette + 2-bit codes of each frame's LLRs (one workgroup per frame).  Wave 0
 // collects up to 4 distinct values (bitwise) in first-occurrence order; a frame
-// with more gets pal_ok = 0 and the decoder gathers its llr[] instead.
+// with more gets pal_ok = 0 and the decoder gathers its llr[] instead.  Unused
+// entries repeat entry 0 (the SPA iteration-0 test reads all four).
 __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const double *llr, uint8_t *codes,
                                                         double *palette, uint8_t *pal_ok) {
     __shared__ unsigned long long pv[4];
@@ -620,7 +709,7 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
             }
         }
         if (threadIdx.x == 0) {
-            for (int q = 0; q < 4; ++q) pv[q] = p[q];
+            for (int q = 0; q < 4; ++q) pv[q] = (q < cnt) ? p[q] : p[0];  // unused entries repeat entry 0
             pcount = cnt;
             over = overflow ? 1 : 0;
         }

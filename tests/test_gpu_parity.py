@@ -148,6 +148,27 @@ def test_c2_unpaletted_llrs(gpu_available, alg, prim, sec):
     assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0, batch=16, llr=llr, synd=s)
 
 
+@pytest.mark.parametrize("name,batch", [("c1_n1024_m220.alist", 24), ("c2_n10240_m2201.alist", 8),
+                                        ("c4s_n102400_m32001.alist", 4)])
+def test_spa_iteration0_uniform_llr_table(gpu_available, name, batch):
+    """SPA iteration 0 on +-L frames takes per-frame tables (t0, A[d]) instead
+    of per-edge tanh/atanh: both ends of its L range, L past the tanh
+    saturation (t0 = 1, messages = +-thr), threshold off, iteration caps 1-3
+    and an all-positive frame (one-entry palette).  Outside the range (and
+    with a third LLR value) the general pass runs; results must agree."""
+    H = load_fixture(name)
+    a, b, _, s = frames(H, 0.03, batch, 90)
+    sign = np.where(b != 0, -1.0, 1.0)
+    sign[0] = 1.0  # no channel errors in frame 0
+    for L in (2.0**-20, 2.0**-21, 0.37, 3.5, 43.99, 44.0, 60.0, 2.0**10, 2.0**10 * 1.5):
+        for max_it, thr_on in ((1, True), (2, True), (3, False), (12, True)):
+            assert_parity(name, Q.SPA, 0, 0, qber=0, batch=batch, max_it=max_it, thr_on=thr_on,
+                          llr=sign * L, synd=s)
+    llr = sign * 2.5
+    llr[1, 7] = 1e-4  # a third value: general iteration 0 for that frame only
+    assert_parity(name, Q.SPA, 0, 0, qber=0, batch=batch, max_it=8, llr=llr, synd=s)
+
+
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c2_rate_adapted_palette(gpu_available, alg, prim, sec):
     """Punctured (1e-4) and shortened (DBL_MAX) positions on the V2 kernel: four
