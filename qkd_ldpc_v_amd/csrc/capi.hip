@@ -506,9 +506,10 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // (descending) so each term's bits are a prefix: stage[off[kk] + rank[b]].
     g->vn_k0 = g->dv_max;
     std::vector<int32_t> hd_bits, hd_dv, stage_off(std::max(1, g->dv_max), 0), rank(n, -1);
-    // (split frames: every term after the first goes through the stage)
-    if (v2 && ((g->v2RG > 0 && g->dv_max > 4) || (g->split_k > 1 && g->dv_max > 1))) {
-        g->vn_k0 = g->split_k > 1 ? 1 : 4;
+    // (split frames: every term goes through the stage, and the gather pass
+    // adds them to the channel LLR in order: the message pass stores only)
+    if (v2 && ((g->v2RG > 0 && g->dv_max > 4) || (g->split_k > 1 && g->dv_max >= 1))) {
+        g->vn_k0 = g->split_k > 1 ? 0 : 4;
         for (int i = 0; i < n; ++i)
             if (dv[i] > g->vn_k0) hd_bits.push_back(i);
         std::stable_sort(hd_bits.begin(), hd_bits.end(), [&](int x, int y) { return dv[x] > dv[y]; });

@@ -211,6 +211,33 @@ struct MetaSrcW : MetaSrc<R> {
             }
         }
     }
+    // Same, with a per-slot value ld(mt) (a total in global memory) loaded for
+    // the group's four slots before any of them is visited, and the next
+    // group's metadata requested before this group's work: one memory latency
+    // per group instead of two per slot.
+    template <typename LD, typename F>
+    __device__ __forceinline__ void each_upto_tv(int epl_s, LD &&ld, F &&f) const {
+        asm volatile("" : "+s"(epl_s));
+        auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            rotate_prio(g);
+            if (4 * g < epl_s) {
+                double tv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) tv[i] = ld((uint32_t)q[i]);  // slots past epl: dummy column
+                const auto qn = (g + 1 < R / 4)
+                                    ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff,
+                                                                            (g + 1) * REG_TSTRIDE * 16, 0)
+                                    : q;
+                f(4 * g + 0, (uint32_t)q[0], tv[0]);
+                if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1], tv[1]);
+                if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2], tv[2]);
+                if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3], tv[3]);
+                q = qn;
+            }
+        }
+    }
     // Same as each_upto, also handing over the word of a second metadata array
     // of identical layout (rs2).
     template <typename F>

@@ -340,9 +340,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         auto emit = [&](int k, uint32_t mt, uint32_t mt2, double c) {
             c2b.set(k, c);
             const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-            if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
-                const int col = (int)(mt & META_COL_MASK);
-                total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
+            if constexpr (!SPLIT) {
+                if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
+                    const int col = (int)(mt & META_COL_MASK);
+                    total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
+                }
             }
             if constexpr (GATHER) {
                 if (kp >= (uint32_t)k0 && kp != 63u) {
@@ -397,7 +399,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         }
                         double sacc[4];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) sacc[j] = (b[j] >= 0) ? total[b[j]] : 0.0;
+                        for (int j = 0; j < 4; ++j) {
+                            // split frames stage every term: the sum starts at the channel LLR
+                            if constexpr (SPLIT) sacc[j] = (b[j] >= 0) ? llr_of(b[j]) : 0.0;
+                            else sacc[j] = (b[j] >= 0) ? total[b[j]] : 0.0;
+                        }
                         for (int kk = k0; kk < a.dv_max; ++kk) {
                             const int off = a.stage_off[kk];
                             double v[4];
@@ -489,9 +495,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             int div_unsafe = 0;
             uint32_t zt = 0;  // decisions of the first KT slots (tail parity)
             double acc = 1.0, m1 = DBL_MAX, m2 = DBL_MAX;
-            meta.each_upto(epl, [&](int k, uint32_t mt) {
-                const int col = (int)(mt & META_COL_MASK);
-                const double tv = total[col];
+            auto scan_slot = [&](int k, uint32_t mt, double tv) {
                 const int zb = (tv <= 0.0) ? 1 : 0;
                 if (k < KT) zt |= (uint32_t)zb << k;
                 const bool start = (mt & META_START) != 0;
@@ -550,7 +554,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         rowflag[r] = (uint8_t)(cur_s | (mr << 1) | (neg << 2));
                     }
                 }
-            });
+            };
+            if constexpr (SPLIT) {  // totals in global memory: a group's four loads issued together
+                meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
+            } else {
+                meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, total[(int)(mt & META_COL_MASK)]); });
+            }
             // ---- rows split across two lanes of this wave: one shuffle ----
             {
                 const int ppar = __shfl(par, up, 64);
