@@ -171,7 +171,7 @@ int block_threads(const qldpc_graph &g) {
 
 size_t lds_of(const qldpc_graph &g, int alg) {
     if (g.variant == VAR_V2 && g.split_k > 1) return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true);
-    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T) : lds_bytes_for(g.variant, g.n, g.m, g.T);
+    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG) : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
 int env_int(const char *name, int dflt) {

@@ -34,6 +34,9 @@ constexpr int V2_R_TIGHT = 40, V2_R_SMALL = 44, V2_R_MID = 56;
 constexpr int V2_CODES_CAP = 20480;  // V2: bits per frame whose palette indices fit LDS (n <= this)
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;
+// SPA-family register kernels at V2_R_TIGHT keep this many message slots in LDS
+// (when the frame's LDS image leaves room) instead of VGPRs.
+constexpr int V2_RL = 4;
 // Workgroup size each V2 instantiation is compiled for (its VGPR budget).
 constexpr __host__ __device__ int v2_threads_for(int R) { return R <= V2_R_SMALL ? 1024 : 768; }
 
@@ -126,7 +129,8 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
                                hipStream_t stream);
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false);
+// LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0);
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,

@@ -105,28 +105,40 @@ struct EdgeMsgs<0> {  // per-workgroup global scratch, slot-major [k][lane]: coa
     __device__ __forceinline__ void set(int k, double x) { p[(size_t)k * T] = x; }
 };
 
-// V2 message storage: slots k < R in VGPRs, slots R <= k < R + RG in this
-// workgroup's global scratch, slot-major [k - R][lane] (lane stride
-// REG_TSTRIDE) — coalesced, constant offsets, L2/MALL-resident.  A lane only
-// ever reads back what it wrote itself, so program order suffices.
-template <int R, int RG>
+// V2 message storage: slots k < R - RL in VGPRs, slots R - RL <= k < R in
+// LDS, slot-major [k - (R - RL)][lane] (lane stride REG_TSTRIDE: conflict-free
+// 8-byte rows, constant offsets from one base register), and slots
+// R <= k < R + RG in this workgroup's global scratch, slot-major [k - R][lane]
+// — coalesced, constant offsets, L2/MALL-resident.  A lane only ever reads
+// back what it wrote itself, so program order suffices.  The LDS slots keep
+// the register kernel within 128 VGPRs without compiler spills (scratch
+// stores whose reloads wait on the vector-memory counter).
+template <int R, int RG, int RL = 0>
 struct EdgeMsgsH {
-    double v[R];
+    static constexpr int RV = R - RL;
+    double v[RV];
     __amdgpu_buffer_rsrc_t rs;
     int voff;
+    double *lp;
     __device__ __forceinline__ void bind(double *wg_base, int tid) {
         if constexpr (RG > 0) {
             rs = __builtin_amdgcn_make_buffer_rsrc((void *)wg_base, (short)0, RG * REG_TSTRIDE * 8, 0x00020000);
             voff = tid * 8;
         }
     }
+    __device__ __forceinline__ void bind_lds(double *lds_base, int tid) {
+        if constexpr (RL > 0) lp = lds_base + tid;
+    }
     __device__ __forceinline__ double get(int k) const {
-        if (k < R) return v[k];
+        if (k < RV) return v[k];
+        if (k < R) return lp[(k - RV) * REG_TSTRIDE];
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (k - R) * REG_TSTRIDE * 8, 0));
     }
     __device__ __forceinline__ void set(int k, double x) {
-        if (k < R) {
+        if (k < RV) {
             v[k] = x;
+        } else if (k < R) {
+            lp[(k - RV) * REG_TSTRIDE] = x;
         } else {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), rs, voff, (k - R) * REG_TSTRIDE * 8,

@@ -45,8 +45,8 @@ constexpr int V2_A0_ENTRIES = 64;
 // memory and the palette indices are read from the 2-bit global codes; LDS
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
-    size_t total, rows, rowflag, tail, tailneg, a0tab, codes, palette, bytes;
-    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false) {
+    size_t total, rows, rowflag, tail, tailneg, a0tab, msl, codes, palette, bytes;
+    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
@@ -56,6 +56,7 @@ struct V2Layout {
         tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
         tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
+        msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         bytes = o;
     }
 };
@@ -72,10 +73,17 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 // SPLIT: a frame is decoded by a.split_k workgroups of one XCD (planner
 // parts: contiguous blocks of 16 waves' rows), which meet at every phase
 // boundary through a global arrival counter; totals are in global memory.
-template <bool SPLIT>
+template <bool SPLIT, int RL>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true);
-    else return V2Layout(a.n, a.m, a.nc, a.T, minsum);
+    else return V2Layout(a.n, a.m, a.nc, a.T, minsum, false, RL);
+}
+
+// Whether a launch runs the LDS-slot instantiation (RL = V2_RL): SPA family,
+// register shape V2_R_TIGHT, and the frame's LDS image plus the slots fit.
+__host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, int n, int m, int T) {
+    if (alg > 1 || R != V2_R_TIGHT || RG != 0 || split || T > REG_TSTRIDE) return false;
+    return V2Layout(n, m, (n + 3) / 4, T, false, false, V2_RL).bytes <= 160 * 1024;
 }
 
 constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
@@ -101,7 +109,7 @@ __device__ __forceinline__ void group_sync(int *ctr, int target, int *err) {
     asm volatile("buffer_inv sc1" ::: "memory");
 }
 
-template <int ALG, int R, int RG, bool SPLIT>
+template <int ALG, int R, int RG, bool SPLIT, int RL = 0>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
@@ -121,7 +129,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // threshold_matrix disabled == clipping at +inf (|v| > inf never holds; NaN passes)
     const double thr = a.thr_on ? a.thr : __builtin_inf();
     const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
-    const V2Layout L = v2_layout<SPLIT>(a, !SPA_FAM);
+    const V2Layout L = v2_layout<SPLIT, RL>(a, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
     int *s_part = reinterpret_cast<int *>(smem) + 2;  // SPLIT: rank, sync slot
@@ -137,8 +145,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
     uint8_t *codes = smem + V2_CODES_OFF;
 
-    EdgeMsgsH<R, RG> c2b;
+    EdgeMsgsH<R, RG, RL> c2b;
     c2b.bind(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles, tid);
+    c2b.bind_lds(reinterpret_cast<double *>(smem + L.msl), tid);
     MetaSrcW<S> meta;
     meta.init(a.slot_meta, tid, T);
     // VN phase kk visits only the slots where some lane of this wave holds the
@@ -756,8 +765,9 @@ KernelFn pick_v2(int alg) {
     }
 }
 
-KernelFn kernel_v2(int R, int RG, int split_k, int alg) {
+KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
     if (split_k > 1) return pick_v2<V2_R_TIGHT, 0, true>(alg);
+    if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, false, V2_RL> : decode_v2_kernel<1, V2_R_TIGHT, 0, false, V2_RL>;
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
     if (R == V2_R_TIGHT) return pick_v2<V2_R_TIGHT, 0>(alg);
     if (R == V2_R_SMALL) return pick_v2<V2_R_SMALL, 0>(alg);
@@ -766,12 +776,14 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split) {
-    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, split).bytes;
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG) {
+    const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
+    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0).bytes;
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
-    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg);
+    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
+                           v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
@@ -780,7 +792,7 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 }
 
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
-    KernelFn k = kernel_v2(R, RG, split_k, alg);
+    KernelFn k = kernel_v2(R, RG, split_k, alg, false);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
