@@ -87,6 +87,7 @@ struct DeviceGraph {
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
     int32_t *part_row0 = nullptr; // V2 split: first layout row of each part
     int32_t *iso_bits = nullptr;
+    uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n][2] four u16 layout rows per bit
     std::mutex mu;
     std::map<void *, Workspace> ws;
     HostIO io;
@@ -587,6 +588,20 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         return QLDPC_OK;
     };
     std::vector<int32_t> row_orig(v2 ? g->row_order : std::vector<int>());
+    // Min-sum bit gather (VNG): per bit, the layout rows of its kpos-th edge,
+    // u16 each, 0xFFFF past its degree.
+    std::vector<uint32_t> vn_rows;
+    if (v2 && v2_vng_ok(2, g->v2R, g->v2RG, g->split_k, g->dv_max, m)) {
+        vn_rows.assign((size_t)2 * n, 0xFFFFFFFFu);
+        for (int j = 0; j < m; ++j) {
+            const int r = g->row_order[j];
+            for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                uint32_t &w = vn_rows[(size_t)2 * col_idx[e] + (kpos[e] >> 1)];
+                const int sh = 16 * (kpos[e] & 1);
+                w = (w & ~(0xFFFFu << sh)) | ((uint32_t)j << sh);
+            }
+        }
+    }
     std::vector<uint32_t> meta_ms, meta2, meta2_ms;
     std::vector<uint64_t> vnm, vnm_ms, vex, vex_ms;
     int brc = build_meta(false, meta, vnm, meta2, vex);
@@ -646,7 +661,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->lane_row0, lrow0)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
-            (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso))) {
+            (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso)) ||
+            (rc = upload(&dg->vn_rows, vn_rows))) {
             (void)hipSetDevice(prev);
             return rc;
         }
@@ -810,6 +826,12 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.nc = (g->n + 3) / 4;
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
     a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
+    {  // min-sum bit gather where the shape allows it (QLDPC_VNG=0: VN phases instead)
+        const char *e = std::getenv("QLDPC_VNG");
+        const bool off = e && std::strcmp(e, "0") == 0;
+        if (v2 && dg->vn_rows && !off && v2_vng_ok(alg, g->v2R, g->v2RG, a.split_k, g->dv_max, g->m))
+            a.vn_rows = reinterpret_cast<const uint2 *>(dg->vn_rows);
+    }
     if (v2 && !codes_ready)
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
@@ -951,6 +973,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->ell_col);
         (void)hipFree(d->row_deg);
         (void)hipFree(d->iso_bits);
+        (void)hipFree(d->vn_rows);
         for (auto &kv : d->ws) {
             (void)hipFree(kv.second.counter);
             (void)hipFree(kv.second.scratch);

@@ -112,6 +112,10 @@ struct DecodeArgs {
     int *split_err;                 // set when a part group failed to meet (results void)
     double *gstage;                 // [batch][stage_frame_doubles] split frames' VN stage
     long long stage_frame_doubles;
+    // V2 min-sum bit gather (VNG, dv_max <= 4): the message pass records per
+    // edge two bits (b2c <= 0, |b2c| == min1) in LDS, and one pass per bit
+    // rebuilds its messages from its rows' aggregates and sums them in order.
+    const uint2 *vn_rows;           // [n]: four u16 layout rows per bit, kpos order (0xFFFF: none); null: off
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -131,6 +135,8 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0);
+// Whether a V2 launch runs the min-sum bit gather (DecodeArgs::vn_rows).
+bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m);
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,

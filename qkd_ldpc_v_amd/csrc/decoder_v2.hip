@@ -109,7 +109,13 @@ __device__ __forceinline__ void group_sync(int *ctr, int target, int *err) {
     asm volatile("buffer_inv sc1" ::: "memory");
 }
 
-template <int ALG, int R, int RG, bool SPLIT, int RL = 0>
+// VNG (min-sum family, dv_max <= 4, not split): no VN phases.  The message
+// pass ORs two bits per edge into a per-bit byte in LDS (the palette-index
+// area: the channel LLR is then read from the frame's 2-bit global codes);
+// after one barrier each thread rebuilds a bit's messages from its rows'
+// aggregates — the same operations the message pass ran — and sums them in
+// kpos order onto the channel LLR (std::accumulate order, :78).
+template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
@@ -122,6 +128,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // high-degree terms, and on split frames every term after the first (the
     // totals are global there anyway; the gather reads the stage coalesced).
     constexpr bool GATHER = RG > 0 || SPLIT;
+    static_assert(!VNG || (!SPA_FAM && !GATHER), "VNG: min-sum family, register shapes");
     constexpr int KT = v2_tail_slots<S>();
 
     const int tid = threadIdx.x;
@@ -171,7 +178,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, GATHER ? 0x7fffffff : 0, 0x00020000);
     __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.slot_meta2, (short)0, GATHER ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
-    const int k0 = GATHER ? a.vn_k0 : a.dv_max;
+    const int k0 = GATHER ? a.vn_k0 : (VNG ? 1 : a.dv_max);
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
     const int head_in0 = a.lane_head[tid];
@@ -286,6 +293,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const uint8_t *gcodes = a.codes + (size_t)f * nc;
         if constexpr (SPLIT) {
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
+        } else if constexpr (VNG) {
+            // the per-bit edge-code bytes start cleared (the gather re-clears them)
+            uint32_t *codes4 = reinterpret_cast<uint32_t *>(codes);
+            for (int i = tid; i < nc; i += T) codes4[i] = 0u;
+            if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
         } else {
             // 2-bit codes -> one byte per bit (the message pass's llr lookup is
             // then a byte read, no shift/mask arithmetic)
@@ -301,7 +313,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
         auto llr_of = [&](int col) -> double {
-            if constexpr (SPLIT) {
+            if constexpr (SPLIT || VNG) {
                 if (paletted) return pal[(gcodes[col >> 2] >> ((col & 3) * 2)) & 3];
             } else {
                 if (paletted) return pal[codes[col]];
@@ -344,12 +356,31 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 #pragma unroll
             for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
         }
+        // Min-sum check-to-bit message of layout row r to an edge whose b2c x
+        // has sign bit xneg = (x > 0 ? 0 : 1) and eq1 = (|x| == min1), clipped
+        // (:73-74).  Shared by the message pass and the VNG bit gather.
+        auto ms_message = [&](double2 ab, int fl, uint32_t xneg, bool eq1) -> double {
+            // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
+            const int sb = (fl ^ (fl >> 2) ^ (int)xneg) & 1;
+            const double prod = sb ? -1. : 1.;
+            const double sel = eq1 ? ab.y : ab.x;  // :406
+            double fac = a.primary;
+            if (ADAPT && (fl & 2)) fac = a.secondary;  // :749-757
+            double c;
+            if constexpr (NORM) {
+                c = fac * prod * sel;
+            } else {
+                const double d = sel - fac;
+                c = prod * ((d < 0.) ? 0. : d);
+            }
+            return clip_msg(c, thr);
+        };
         // Message emission shared by both message passes: c2b, VN phase 0
         // (total = llr + first message) and the hybrid/split VN stage.
         auto emit = [&](int k, uint32_t mt, uint32_t mt2, double c) {
             c2b.set(k, c);
             const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-            if constexpr (!SPLIT) {
+            if constexpr (!SPLIT && !VNG) {
                 if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
                     const int col = (int)(mt & META_COL_MASK);
                     total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
@@ -387,6 +418,30 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
                             total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
                 });
+                STAMP(ST_VNK);
+                psync();
+                STAMP(ST_VNK_WAIT);
+            }
+            if constexpr (VNG) {
+                // every bit: its dv <= 4 messages rebuilt in kpos order and summed
+                // onto the channel LLR; the next bit's rows are requested first
+                const uint2 *vr = a.vn_rows;
+                uint2 rr = (tid < n) ? vr[tid] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+                for (int b = tid; b < n; b += T) {
+                    const uint2 cur = rr;
+                    if (b + T < n) rr = vr[b + T];
+                    const uint32_t cb = codes[b];
+                    codes[b] = 0;
+                    double sacc = llr_of(b);
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const uint32_t r = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
+                        if (r != 0xFFFFu)
+                            sacc = sacc + ms_message(rowAB[r], rowflag[r], (cb >> (2 * kk)) & 1u,
+                                                     ((cb >> (2 * kk)) & 2u) != 0);
+                    }
+                    total[b] = sacc;
+                }
                 STAMP(ST_VNK);
                 psync();
                 STAMP(ST_VNK_WAIT);
@@ -642,22 +697,22 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     c = 2. * atanh_lin(prod);
                 } else {
                     const double x = c2b.get(k);
+                    const uint32_t xneg = (x > 0) ? 0u : 1u;
                     const double2 ab = rowAB[r];
-                    const int fl = rowflag[r];
-                    // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
-                    const int sb = (fl ^ (fl >> 2) ^ ((x > 0) ? 0 : 1)) & 1;
-                    const double prod = sb ? -1. : 1.;
-                    const double sel = (__builtin_fabs(x) == ab.x) ? ab.y : ab.x;  // :406
-                    double fac = a.primary;
-                    if (ADAPT && (fl & 2)) fac = a.secondary;  // :749-757
-                    if constexpr (NORM) {
-                        c = fac * prod * sel;
-                    } else {
-                        const double d = sel - fac;
-                        c = prod * ((d < 0.) ? 0. : d);
+                    const bool eq1 = __builtin_fabs(x) == ab.x;
+                    c = ms_message(ab, rowflag[r], xneg, eq1);
+                    if constexpr (VNG) {
+                        // record the two bits the bit gather rebuilds this message from
+                        const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
+                        if (kp < 4u) {  // (dummy slots: kpos 63)
+                            const int col = (int)(mt & META_COL_MASK);
+                            __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes) + (col >> 2),
+                                                  (xneg | (eq1 ? 2u : 0u)) << (((col & 3) << 3) + 2 * kp),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
                     }
                 }
-                if constexpr (ALG != 0) c = clip_msg(c, thr);  // (:73-74)
+                if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 emit(k, mt, mt2, c);
             };
             if constexpr (GATHER) {
@@ -765,6 +820,15 @@ KernelFn pick_v2(int alg) {
     }
 }
 
+KernelFn kernel_v2_vng(int alg) {
+    switch (alg) {
+    case 2: return decode_v2_kernel<2, V2_R_TIGHT, 0, false, 0, true>;
+    case 3: return decode_v2_kernel<3, V2_R_TIGHT, 0, false, 0, true>;
+    case 4: return decode_v2_kernel<4, V2_R_TIGHT, 0, false, 0, true>;
+    default: return decode_v2_kernel<5, V2_R_TIGHT, 0, false, 0, true>;
+    }
+}
+
 KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
     if (split_k > 1) return pick_v2<V2_R_TIGHT, 0, true>(alg);
     if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, false, V2_RL> : decode_v2_kernel<1, V2_R_TIGHT, 0, false, V2_RL>;
@@ -781,9 +845,15 @@ size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG) {
     return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0).bytes;
 }
 
+bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
+    return alg >= 2 && R == V2_R_TIGHT && RG == 0 && split_k <= 1 && dv_max <= 4 && m < 0xFFFF;
+}
+
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
-    KernelFn k = kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
-                           v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
+    if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
+    KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg)
+                           : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
+                                       v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;

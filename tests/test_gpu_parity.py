@@ -199,6 +199,18 @@ def test_c3_10k(gpu_available, alg, prim, sec):
     assert_parity("c3_n10240_m1801.alist", alg, prim, sec, qber=0.015, batch=32, seed=10022025)
 
 
+@pytest.mark.parametrize("vng", ["1", "0"])
+@pytest.mark.parametrize("alg,prim,sec", ALGS[2:])
+def test_minsum_bit_gather_and_vn_phases(gpu_available, alg, prim, sec, vng, monkeypatch):
+    """Min-sum family on dv <= 4 codes: the bit gather (default, messages
+    rebuilt per bit from row aggregates) and the VN-phase path (QLDPC_VNG=0,
+    read per launch) both bit-exact, incl. iteration caps and threshold off."""
+    monkeypatch.setenv("QLDPC_VNG", vng)
+    assert_parity("c3_n10240_m1801.alist", alg, prim, sec, qber=0.02, batch=24, seed=77)
+    assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.03, batch=16, seed=78, max_it=3)
+    assert_parity("c1_n1024_m220.alist", alg, prim, sec, qber=0.04, batch=32, seed=79, thr_on=False)
+
+
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
     assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
