@@ -52,7 +52,7 @@ struct V2Layout {
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
         total = o; o = split ? o : al16(o + (size_t)(n + 1) * 8);
         rows = o; o = al16(o + (size_t)m * (minsum ? 16 : 8));  // SPA: product; min-sum: {min1, min2}
-        rowflag = o; o = al16(o + (minsum ? (size_t)m : 0));
+        rowflag = o;  // (min-sum row flags ride in the sign bits of rowAB: none here)
         tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
         tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
@@ -143,10 +143,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     double *total = reinterpret_cast<double *>(smem + V2_TOTAL_OFF);
     double *const rowA_lds = reinterpret_cast<double *>(smem + L.rows);    // SPA
     double2 *const rowAB_lds = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
-    uint8_t *const rowflag_lds = smem + L.rowflag;  // min-sum: bit0 syndrome, bit1 row mismatch, bit2 negative parity
     double *rowA = rowA_lds;
     double2 *rowAB = rowAB_lds;
-    uint8_t *rowflag = rowflag_lds;
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
     double2 *tailagg = reinterpret_cast<double2 *>(smem + L.tail);
     int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
@@ -252,7 +250,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             const int rb = a.part_row0[rank];
             rowA = rowA_lds - rb;
             rowAB = rowAB_lds - rb;
-            rowflag = rowflag_lds - rb;
             total = a.gtotal + (size_t)f * (n + 1);
             stage = a.gstage + (size_t)f * a.stage_frame_doubles;
             stage_rs = __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, 0x7fffffff, 0x00020000);
@@ -356,16 +353,23 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 #pragma unroll
             for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
         }
+        auto ms_pack = [](double m1, double m2, int sgn, int mr) -> double2 {
+            return make_double2(__builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m1) | ((uint64_t)(sgn & 1) << 63)),
+                                __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m2) | ((uint64_t)(mr & 1) << 63)));
+        };
         // Min-sum check-to-bit message of layout row r to an edge whose b2c x
         // has sign bit xneg = (x > 0 ? 0 : 1) and eq1 = (|x| == min1), clipped
         // (:73-74).  Shared by the message pass and the VNG bit gather.
-        auto ms_message = [&](double2 ab, int fl, uint32_t xneg, bool eq1) -> double {
+        // Row aggregate {min1, min2} (both >= +0) with the row's sign s xor
+        // (parity of negative b2c) in min1's sign bit and its syndrome
+        // mismatch (the adaptive factor's selector) in min2's.
+        auto ms_message = [&](double2 ab, uint32_t xneg, bool eq1) -> double {
             // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
-            const int sb = (fl ^ (fl >> 2) ^ (int)xneg) & 1;
+            const uint32_t sb = (ql_exact::hi_word(ab.x) >> 31) ^ xneg;
             const double prod = sb ? -1. : 1.;
-            const double sel = eq1 ? ab.y : ab.x;  // :406
+            const double sel = eq1 ? __builtin_fabs(ab.y) : __builtin_fabs(ab.x);  // :406
             double fac = a.primary;
-            if (ADAPT && (fl & 2)) fac = a.secondary;  // :749-757
+            if (ADAPT && (ql_exact::hi_word(ab.y) >> 31)) fac = a.secondary;  // :749-757
             double c;
             if constexpr (NORM) {
                 c = fac * prod * sel;
@@ -437,7 +441,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     for (int kk = 0; kk < 4; ++kk) {
                         const uint32_t r = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
                         if (r != 0xFFFFu)
-                            sacc = sacc + ms_message(rowAB[r], rowflag[r], (cb >> (2 * kk)) & 1u,
+                            sacc = sacc + ms_message(rowAB[r], (cb >> (2 * kk)) & 1u,
                                                      ((cb >> (2 * kk)) & 2u) != 0);
                     }
                     total[b] = sacc;
@@ -614,8 +618,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         rowA[r] = acc;
                         if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
                     } else {
-                        rowAB[r] = make_double2(m1, m2);
-                        rowflag[r] = (uint8_t)(cur_s | (mr << 1) | (neg << 2));
+                        rowAB[r] = ms_pack(m1, m2, cur_s ^ neg, mr);
                     }
                 }
             };
@@ -652,8 +655,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         h.neg = tailneg[tid];
                         agg_merge(t, h);
                         const int mr = ppar ^ hpar ^ s_row0;
-                        rowAB[row0] = make_double2(t.m1, t.m2);
-                        rowflag[row0] = (uint8_t)(s_row0 | (mr << 1) | (t.neg << 2));
+                        rowAB[row0] = ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr);
                         mis |= mr;
                     }
                 }
@@ -699,8 +701,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const double x = c2b.get(k);
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
                     const double2 ab = rowAB[r];
-                    const bool eq1 = __builtin_fabs(x) == ab.x;
-                    c = ms_message(ab, rowflag[r], xneg, eq1);
+                    const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
+                    c = ms_message(ab, xneg, eq1);
                     if constexpr (VNG) {
                         // record the two bits the bit gather rebuilds this message from
                         const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
