@@ -428,21 +428,44 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             }
             if constexpr (VNG) {
                 // every bit: its dv <= 4 messages rebuilt in kpos order and summed
-                // onto the channel LLR; the next bit's rows are requested first
+                // onto the channel LLR.  The next bit's rows and channel code are
+                // requested before this bit's work (nothing here waits on them),
+                // and a bit's four row aggregates are read together (missing
+                // terms read row 0 and are not added).
                 const uint2 *vr = a.vn_rows;
-                uint2 rr = (tid < n) ? vr[tid] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-                for (int b = tid; b < n; b += T) {
+                int b = tid;
+                uint2 rr = make_uint2(0u, 0u);
+                uint32_t gcn = 0;
+                double lrn = 0.0;
+                if (b < n) {
+                    rr = vr[b];
+                    if (paletted) gcn = gcodes[b >> 2];
+                    else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, b * 8, 0, 0));
+                }
+                for (; b < n; b += T) {
                     const uint2 cur = rr;
-                    if (b + T < n) rr = vr[b + T];
+                    const uint32_t gc = gcn;
+                    const double lr = lrn;
+                    const int bn = b + T;
+                    if (bn < n) {
+                        rr = vr[bn];
+                        if (paletted) gcn = gcodes[bn >> 2];
+                        else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, bn * 8, 0, 0));
+                    }
                     const uint32_t cb = codes[b];
                     codes[b] = 0;
-                    double sacc = llr_of(b);
+                    uint32_t rk[4];
+                    double2 ab[4];
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk) {
-                        const uint32_t r = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
-                        if (r != 0xFFFFu)
-                            sacc = sacc + ms_message(rowAB[r], (cb >> (2 * kk)) & 1u,
-                                                     ((cb >> (2 * kk)) & 2u) != 0);
+                        rk[kk] = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
+                        ab[kk] = rowAB[rk[kk] != 0xFFFFu ? (int)rk[kk] : 0];
+                    }
+                    double sacc = paletted ? pal[(gc >> ((b & 3) * 2)) & 3u] : lr;
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const double c = ms_message(ab[kk], (cb >> (2 * kk)) & 1u, ((cb >> (2 * kk)) & 2u) != 0);
+                        sacc = (rk[kk] != 0xFFFFu) ? sacc + c : sacc;
                     }
                     total[b] = sacc;
                 }
