@@ -87,7 +87,8 @@ struct DeviceGraph {
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
     int32_t *part_row0 = nullptr; // V2 split: first layout row of each part
     int32_t *iso_bits = nullptr;
-    uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n][2] four u16 layout rows per bit
+    uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
+    uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
     std::mutex mu;
     std::map<void *, Workspace> ws;
     HostIO io;
@@ -143,6 +144,7 @@ struct Xoshiro256pp {
 
 struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
+    bool vng = false;                       // V2 min-sum bit gather tables built
     int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
     std::vector<int> wave_rows;             // V2: first layout row of each wave (+ m)
     std::vector<int> row_order;             // V2: layout row -> original row
@@ -527,6 +529,50 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     }
     g->n_hd = (int)hd_bits.size();
     const int S4 = G4 * 4;  // V2 slots per lane (register + scratch)
+    // Min-sum bit gather (VNG).  Register shape, dv <= 4: per bit, the layout
+    // rows of its kpos-th edge (u16 each, 0xFFFF past its degree).  Hybrid
+    // shape: a bit's edges padded to chunks of four (position P0[b] + kpos),
+    // rows per chunk (padding: row 0), each slot's position (vng_meta2; dummy
+    // slots: a scratch chunk per lane past the last), bits in degree order.
+    std::vector<uint32_t> vn_rows, vng_bits, vng_meta2;
+    long long vng_chunks = 0;
+    std::vector<long long> P0(v2 ? n : 0, 0);
+    if (v2 && v2_vng_ok(2, g->v2R, g->v2RG, g->split_k, g->dv_max, m)) {
+        std::vector<int> lrow_of(m, 0);
+        for (int j = 0; j < m; ++j) lrow_of[g->row_order[j]] = j;
+        if (g->v2RG == 0) {
+            vn_rows.assign((size_t)2 * n, 0xFFFFFFFFu);
+            for (int r = 0; r < m; ++r)
+                for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                    uint32_t &w = vn_rows[(size_t)2 * col_idx[e] + (kpos[e] >> 1)];
+                    const int sh = 16 * (kpos[e] & 1);
+                    w = (w & ~(0xFFFFu << sh)) | ((uint32_t)lrow_of[r] << sh);
+                }
+        } else {
+            for (int b = 0; b < n; ++b) {
+                P0[b] = vng_chunks * 4;
+                vng_chunks += (dv[b] + 3) / 4;
+            }
+            if (vng_chunks + V2_VNG_DUMMY_CHUNKS <= V2_CODES_CAP && g->dv_max < 256) {
+                vn_rows.assign((size_t)2 * vng_chunks, 0u);
+                for (int r = 0; r < m; ++r)
+                    for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                        const long long P = P0[col_idx[e]] + kpos[e];
+                        vn_rows[(size_t)(P >> 1)] |= (uint32_t)lrow_of[r] << (16 * (P & 1));
+                    }
+                std::vector<int> ord(n);
+                for (int b = 0; b < n; ++b) ord[b] = b;
+                std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return dv[x] > dv[y]; });
+                vng_bits.resize((size_t)2 * n);
+                for (int i = 0; i < n; ++i) {
+                    vng_bits[2 * i] = (uint32_t)ord[i];
+                    vng_bits[2 * i + 1] = (uint32_t)(P0[ord[i]] / 4) | ((uint32_t)dv[ord[i]] << 24);
+                }
+                vng_meta2.assign((size_t)G4 * TS * 4 * NPARTS, 0);
+            }
+        }
+    }
+    const bool vng_h = !vng_meta2.empty();
     auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm,
                           std::vector<uint32_t> &mt2, std::vector<uint64_t> &vex) -> int {
         mt.assign((size_t)G4 * TS * 4 * NPARTS, 0);
@@ -561,6 +607,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                     if (k >= epl_w || e >= we) {
                         if (!v2) break;
                         wd = DUMMY;
+                        if (sorted && vng_h) vng_meta2[midx(l, k)] = (uint32_t)((vng_chunks + li) * 4);
                     } else {
                         const int j = lrow[e];
                         const int ed = perm[e];  // the edge at that position
@@ -569,6 +616,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                             vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
                             vex[((size_t)w * g->dv_max + kpos[ed]) * S4 + k] |= 1ull << li;
                         }
+                        if (sorted && vng_h) vng_meta2[midx(l, k)] = (uint32_t)(P0[col_idx[ed]] + kpos[ed]);
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
                             mt2[midx(l, k)] =
                                 (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
@@ -588,20 +636,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         return QLDPC_OK;
     };
     std::vector<int32_t> row_orig(v2 ? g->row_order : std::vector<int>());
-    // Min-sum bit gather (VNG): per bit, the layout rows of its kpos-th edge,
-    // u16 each, 0xFFFF past its degree.
-    std::vector<uint32_t> vn_rows;
-    if (v2 && v2_vng_ok(2, g->v2R, g->v2RG, g->split_k, g->dv_max, m)) {
-        vn_rows.assign((size_t)2 * n, 0xFFFFFFFFu);
-        for (int j = 0; j < m; ++j) {
-            const int r = g->row_order[j];
-            for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
-                uint32_t &w = vn_rows[(size_t)2 * col_idx[e] + (kpos[e] >> 1)];
-                const int sh = 16 * (kpos[e] & 1);
-                w = (w & ~(0xFFFFu << sh)) | ((uint32_t)j << sh);
-            }
-        }
-    }
+    g->vng = !vn_rows.empty();
     std::vector<uint32_t> meta_ms, meta2, meta2_ms;
     std::vector<uint64_t> vnm, vnm_ms, vex, vex_ms;
     int brc = build_meta(false, meta, vnm, meta2, vex);
@@ -662,7 +697,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso)) ||
-            (rc = upload(&dg->vn_rows, vn_rows))) {
+            (rc = upload(&dg->vn_rows, vn_rows)) || (rc = upload(&dg->vng_bits, vng_bits)) ||
+            (rc = upload(&dg->vng_meta2, vng_meta2))) {
             (void)hipSetDevice(prev);
             return rc;
         }
@@ -829,8 +865,13 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     {  // min-sum bit gather where the shape allows it (QLDPC_VNG=0: VN phases instead)
         const char *e = std::getenv("QLDPC_VNG");
         const bool off = e && std::strcmp(e, "0") == 0;
-        if (v2 && dg->vn_rows && !off && v2_vng_ok(alg, g->v2R, g->v2RG, a.split_k, g->dv_max, g->m))
+        if (v2 && g->vng && !off && v2_vng_ok(alg, g->v2R, g->v2RG, a.split_k, g->dv_max, g->m)) {
             a.vn_rows = reinterpret_cast<const uint2 *>(dg->vn_rows);
+            if (g->v2RG > 0) {
+                a.vng_bits = reinterpret_cast<const uint2 *>(dg->vng_bits);
+                a.slot_meta2 = dg->vng_meta2;
+            }
+        }
     }
     if (v2 && !codes_ready)
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
@@ -974,6 +1015,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->row_deg);
         (void)hipFree(d->iso_bits);
         (void)hipFree(d->vn_rows);
+        (void)hipFree(d->vng_bits);
+        (void)hipFree(d->vng_meta2);
         for (auto &kv : d->ws) {
             (void)hipFree(kv.second.counter);
             (void)hipFree(kv.second.scratch);

@@ -116,6 +116,11 @@ struct DecodeArgs {
     // edge two bits (b2c <= 0, |b2c| == min1) in LDS, and one pass per bit
     // rebuilds its messages from its rows' aggregates and sums them in order.
     const uint2 *vn_rows;           // [n]: four u16 layout rows per bit, kpos order (0xFFFF: none); null: off
+    // Hybrid shape (irregular codes): a bit's edges are padded to chunks of
+    // four; vn_rows then holds the rows per chunk ([chunks], padding: row 0),
+    // slot_meta2 each slot's padded edge position, and the gather walks bits
+    // in degree order: vng_bits[i] = {bit, first chunk | dv << 24}.
+    const uint2 *vng_bits;
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -135,8 +140,11 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0);
-// Whether a V2 launch runs the min-sum bit gather (DecodeArgs::vn_rows).
+// Whether a V2 shape can run the min-sum bit gather (DecodeArgs::vn_rows):
+// the dv <= 4 register shape, or the hybrid shape when the padded edge
+// positions' two code bits fit the LDS byte area.
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m);
+constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per lane for dummy slots
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,

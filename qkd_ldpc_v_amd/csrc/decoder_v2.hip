@@ -127,8 +127,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // and summed per bit in one gather pass: the hybrid shape's sparse
     // high-degree terms, and on split frames every term after the first (the
     // totals are global there anyway; the gather reads the stage coalesced).
-    constexpr bool GATHER = RG > 0 || SPLIT;
-    static_assert(!VNG || (!SPA_FAM && !GATHER), "VNG: min-sum family, register shapes");
+    static_assert(!VNG || (!SPA_FAM && !SPLIT), "VNG: min-sum family, one workgroup per frame");
+    constexpr bool GATHER = (RG > 0 || SPLIT) && !VNG;
+    // hybrid bit gather: per-slot padded edge positions in slot_meta2
+    constexpr bool VNG_H = VNG && RG > 0;
     constexpr int KT = v2_tail_slots<S>();
 
     const int tid = threadIdx.x;
@@ -175,7 +177,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     __amdgpu_buffer_rsrc_t stage_rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, GATHER ? 0x7fffffff : 0, 0x00020000);
     __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)a.slot_meta2, (short)0, GATHER ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
+        (void *)a.slot_meta2, (short)0, (GATHER || VNG_H) ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
     const int k0 = GATHER ? a.vn_k0 : (VNG ? 1 : a.dv_max);
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
@@ -293,7 +295,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         } else if constexpr (VNG) {
             // the per-bit edge-code bytes start cleared (the gather re-clears them)
             uint32_t *codes4 = reinterpret_cast<uint32_t *>(codes);
-            for (int i = tid; i < nc; i += T) codes4[i] = 0u;
+            for (int i = tid; i < (VNG_H ? V2_CODES_CAP / 4 : nc); i += T) codes4[i] = 0u;
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
         } else {
             // 2-bit codes -> one byte per bit (the message pass's llr lookup is
@@ -426,7 +428,41 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 psync();
                 STAMP(ST_VNK_WAIT);
             }
-            if constexpr (VNG) {
+            if constexpr (VNG_H) {
+                // every bit, in degree order (a wave's lanes have similar degree):
+                // its messages rebuilt chunk by chunk (four edges: one 8-byte
+                // rows load, one code byte) and summed in kpos order onto the
+                // channel LLR; a chunk's padding reads row 0 and is not added
+                const uint2 *vr = a.vn_rows;
+                for (int i = tid; i < n; i += T) {
+                    const uint2 e = a.vng_bits[i];
+                    const int b = (int)e.x;
+                    const uint32_t c0 = e.y & 0xFFFFFFu;
+                    const int dvb = (int)(e.y >> 24);
+                    double sacc = llr_of(b);
+                    uint2 rr = vr[c0];
+                    for (int kc = 0; kc < dvb; kc += 4) {
+                        const uint32_t ch = c0 + (uint32_t)(kc >> 2);
+                        const uint2 cur = rr;
+                        if (kc + 4 < dvb) rr = vr[ch + 1];
+                        const uint32_t cb = codes[ch];
+                        codes[ch] = 0;
+                        double2 ab[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            ab[q] = rowAB[(int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu)];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const double c = ms_message(ab[q], (cb >> (2 * q)) & 1u, ((cb >> (2 * q)) & 2u) != 0);
+                            sacc = (kc + q < dvb) ? sacc + c : sacc;
+                        }
+                    }
+                    total[b] = sacc;
+                }
+                STAMP(ST_VNK);
+                psync();
+                STAMP(ST_VNK_WAIT);
+            } else if constexpr (VNG) {
                 // every bit: its dv <= 4 messages rebuilt in kpos order and summed
                 // onto the channel LLR.  The next bit's rows and channel code are
                 // requested before this bit's work (nothing here waits on them),
@@ -726,7 +762,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const double2 ab = rowAB[r];
                     const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
                     c = ms_message(ab, xneg, eq1);
-                    if constexpr (VNG) {
+                    if constexpr (VNG_H) {
+                        // the two bits at the edge's padded position (dummy slots:
+                        // a scratch byte past the last chunk)
+                        __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes) + (mt2 >> 4),
+                                              (xneg | (eq1 ? 2u : 0u)) << ((mt2 & 15u) * 2),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else if constexpr (VNG) {
                         // record the two bits the bit gather rebuilds this message from
                         const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
                         if (kp < 4u) {  // (dummy slots: kpos 63)
@@ -740,7 +782,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 emit(k, mt, mt2, c);
             };
-            if constexpr (GATHER) {
+            if constexpr (GATHER || VNG_H) {
                 meta.each_upto2(epl, meta2_rs, message);
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
@@ -845,7 +887,15 @@ KernelFn pick_v2(int alg) {
     }
 }
 
-KernelFn kernel_v2_vng(int alg) {
+KernelFn kernel_v2_vng(int alg, int RG) {
+    if (RG > 0) {
+        switch (alg) {
+        case 2: return decode_v2_kernel<2, V2_R_SMALL, V2_RG_HYBRID, false, 0, true>;
+        case 3: return decode_v2_kernel<3, V2_R_SMALL, V2_RG_HYBRID, false, 0, true>;
+        case 4: return decode_v2_kernel<4, V2_R_SMALL, V2_RG_HYBRID, false, 0, true>;
+        default: return decode_v2_kernel<5, V2_R_SMALL, V2_RG_HYBRID, false, 0, true>;
+        }
+    }
     switch (alg) {
     case 2: return decode_v2_kernel<2, V2_R_TIGHT, 0, false, 0, true>;
     case 3: return decode_v2_kernel<3, V2_R_TIGHT, 0, false, 0, true>;
@@ -871,12 +921,14 @@ size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG) {
 }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
-    return alg >= 2 && R == V2_R_TIGHT && RG == 0 && split_k <= 1 && dv_max <= 4 && m < 0xFFFF;
+    if (alg < 2 || split_k > 1 || m >= 0xFFFF) return false;
+    if (RG == 0) return R == V2_R_TIGHT && dv_max <= 4;
+    return R == V2_R_SMALL && RG == V2_RG_HYBRID;  // + the host's LDS fit test
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
-    KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg)
+    KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
                                        v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),

@@ -209,6 +209,21 @@ def test_minsum_bit_gather_and_vn_phases(gpu_available, alg, prim, sec, vng, mon
     assert_parity("c3_n10240_m1801.alist", alg, prim, sec, qber=0.02, batch=24, seed=77)
     assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.03, batch=16, seed=78, max_it=3)
     assert_parity("c1_n1024_m220.alist", alg, prim, sec, qber=0.04, batch=32, seed=79, thr_on=False)
+    # irregular (dv 2..26) hybrid shape: padded per-bit edge chunks, bits in degree order
+    assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.03, batch=12, seed=80)
+    assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.05, batch=8, seed=81, max_it=2)
+    H = load_fixture("c5_n10240_m2048.sp2")  # rate-adapted style frame: full palette, DBL_MAX, 1e-4
+    rng = np.random.default_rng(82)
+    a, b, llr, s = frames(H, 0.02, 8, 83)
+    pos = rng.permutation(H.n)
+    a[:, pos[300:420]] = 0
+    b[:, pos[300:420]] = 0
+    s = H.syndrome(a)
+    lp = Q.log_p(0.02)
+    llr = np.where(b != 0, -lp, lp)
+    llr[:, pos[:300]] = 1e-4
+    llr[:, pos[300:420]] = DBL_MAX
+    assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0, batch=8, llr=llr, synd=s)
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
