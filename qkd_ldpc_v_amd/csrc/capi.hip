@@ -358,7 +358,11 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr) {
     const long long E = g.E;
     const int R = V2_R_TIGHT, WP = REG_TSTRIDE / 64;
     const long long cap_part = (long long)WP * 64 * R;
-    for (int K = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part); K <= 8; ++K) {
+    // QLDPC_SPLIT_K forces the part count (<= 32: one XCD's CUs)
+    const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
+    const int kforce = env_int("QLDPC_SPLIT_K", 0);
+    if (kforce && (kforce < kmin || kforce > 32)) return false;
+    for (int K = kforce ? kforce : kmin; K <= (kforce ? kforce : 8); ++K) {
         const int W = WP * K;
         const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
         if (cap > 64LL * R) continue;
