@@ -835,6 +835,11 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.alg = alg; a.max_it = p->max_iterations; a.thr_on = p->thr_enabled ? 1 : 0;
     a.thr = p->thr; a.primary = p->primary; a.secondary = p->secondary;
     {
+        const bool norm = alg == 2 || alg == 4, adapt = alg == 4 || alg == 5;
+        const auto fine = [&](double f) { return norm ? (std::fabs(f) <= 1.0) : (f >= 0.0); };  // NaN: not fine
+        a.ms_clip_later = (fine(p->primary) && (!adapt || fine(p->secondary))) ? 0 : 1;
+    }
+    {
         const double lim = (a.thr_on && p->thr < 44.0) ? p->thr : 44.0;
         a.spa_tlim = std::tanh(lim / 2.);
         a.spa_ctop = 2. * std::atanh(0x1.fffffffffffffp-1);

@@ -121,6 +121,9 @@ struct DecodeArgs {
     // slot_meta2 each slot's padded edge position, and the gather walks bits
     // in degree order: vng_bits[i] = {bit, first chunk | dv << 24}.
     const uint2 *vng_bits;
+    // Min-sum: the factor/offset can push |message| above its selected
+    // minimum (|NMSA factor| > 1, negative offset, or NaN): clip every message.
+    int ms_clip_later;
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.

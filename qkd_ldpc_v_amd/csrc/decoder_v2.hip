@@ -16,6 +16,8 @@
 //     DBL_MAX); frames that do not fit gather llr[] from global instead.
 // Per iteration: 1 barrier after the check-node scan, 1 after the message
 // pass, 1 per remaining VN phase (dv_max - 1).
+#include <type_traits>
+
 #include "decoder_common.hpp"
 
 namespace qldpc {
@@ -351,10 +353,17 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
         int iters = a.max_it, okv = 0;
         bool had_vn = false;
-        if constexpr (ALG == 0) {
+        // c2b starts at +0: iteration 0's b2c = tv - 0 with the clip at +inf is
+        // the channel LLR itself, bitwise (the reference's unclipped
+        // initialisation, :21-29), so the scan needs no iteration-0 select
 #pragma unroll
-            for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
-        }
+        for (int k = 0; k < S; ++k) c2b.set(k, 0.0);
+        // Min-sum: after iteration 0 every |b2c| is <= thr, so a message
+        // (|c| <= sel when the offset is >= 0 / the factor is <= 1 in
+        // magnitude: a.ms_clip_later == 0) needs the clip only when some row
+        // kept min2 > thr (rows with < 2 non-NaN b2c): flagged by the scan.
+        bool msclip = a.thr_on != 0;
+        int *s_big = reinterpret_cast<int *>(smem) + 2;  // (non-split only: s_part's slot)
         auto ms_pack = [](double m1, double m2, int sgn, int mr) -> double2 {
             return make_double2(__builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m1) | ((uint64_t)(sgn & 1) << 63)),
                                 __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m2) | ((uint64_t)(mr & 1) << 63)));
@@ -365,7 +374,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // Row aggregate {min1, min2} (both >= +0) with the row's sign s xor
         // (parity of negative b2c) in min1's sign bit and its syndrome
         // mismatch (the adaptive factor's selector) in min2's.
-        auto ms_message = [&](double2 ab, uint32_t xneg, bool eq1) -> double {
+        auto ms_message = [&](double2 ab, uint32_t xneg, bool eq1, bool doclip) -> double {
             // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
             const uint32_t sb = (ql_exact::hi_word(ab.x) >> 31) ^ xneg;
             const double prod = sb ? -1. : 1.;
@@ -379,7 +388,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const double d = sel - fac;
                 c = prod * ((d < 0.) ? 0. : d);
             }
-            return clip_msg(c, thr);
+            if (doclip) c = clip_msg(c, thr);  // (:73-74; a no-op otherwise, see msclip)
+            return c;
         };
         // Message emission shared by both message passes: c2b, VN phase 0
         // (total = llr + first message) and the hybrid/split VN stage.
@@ -433,32 +443,39 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // its messages rebuilt chunk by chunk (four edges: one 8-byte
                 // rows load, one code byte) and summed in kpos order onto the
                 // channel LLR; a chunk's padding reads row 0 and is not added
-                const uint2 *vr = a.vn_rows;
-                for (int i = tid; i < n; i += T) {
-                    const uint2 e = a.vng_bits[i];
-                    const int b = (int)e.x;
-                    const uint32_t c0 = e.y & 0xFFFFFFu;
-                    const int dvb = (int)(e.y >> 24);
-                    double sacc = llr_of(b);
-                    uint2 rr = vr[c0];
-                    for (int kc = 0; kc < dvb; kc += 4) {
-                        const uint32_t ch = c0 + (uint32_t)(kc >> 2);
-                        const uint2 cur = rr;
-                        if (kc + 4 < dvb) rr = vr[ch + 1];
-                        const uint32_t cb = codes[ch];
-                        codes[ch] = 0;
-                        double2 ab[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            ab[q] = rowAB[(int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu)];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const double c = ms_message(ab[q], (cb >> (2 * q)) & 1u, ((cb >> (2 * q)) & 2u) != 0);
-                            sacc = (kc + q < dvb) ? sacc + c : sacc;
+                // (two copies of the loop, with and without the clip: the
+                // uniform msclip picks one by a scalar branch)
+                auto gather_h = [&](auto dct) {
+                    constexpr bool DC = decltype(dct)::value;
+                    const uint2 *vr = a.vn_rows;
+                    for (int i = tid; i < n; i += T) {
+                        const uint2 e = a.vng_bits[i];
+                        const int b = (int)e.x;
+                        const uint32_t c0 = e.y & 0xFFFFFFu;
+                        const int dvb = (int)(e.y >> 24);
+                        double sacc = llr_of(b);
+                        uint2 rr = vr[c0];
+                        for (int kc = 0; kc < dvb; kc += 4) {
+                            const uint32_t ch = c0 + (uint32_t)(kc >> 2);
+                            const uint2 cur = rr;
+                            if (kc + 4 < dvb) rr = vr[ch + 1];
+                            const uint32_t cb = codes[ch];
+                            codes[ch] = 0;
+                            double2 ab[4];
+    #pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                ab[q] = rowAB[(int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu)];
+    #pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const double c = ms_message(ab[q], (cb >> (2 * q)) & 1u, ((cb >> (2 * q)) & 2u) != 0, DC);
+                                sacc = (kc + q < dvb) ? sacc + c : sacc;
+                            }
                         }
+                        total[b] = sacc;
                     }
-                    total[b] = sacc;
-                }
+                };
+                if (msclip) gather_h(std::integral_constant<bool, true>{});
+                else gather_h(std::integral_constant<bool, false>{});
                 STAMP(ST_VNK);
                 psync();
                 STAMP(ST_VNK_WAIT);
@@ -468,43 +485,48 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // requested before this bit's work (nothing here waits on them),
                 // and a bit's four row aggregates are read together (missing
                 // terms read row 0 and are not added).
-                const uint2 *vr = a.vn_rows;
-                int b = tid;
-                uint2 rr = make_uint2(0u, 0u);
-                uint32_t gcn = 0;
-                double lrn = 0.0;
-                if (b < n) {
-                    rr = vr[b];
-                    if (paletted) gcn = gcodes[b >> 2];
-                    else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, b * 8, 0, 0));
-                }
-                for (; b < n; b += T) {
-                    const uint2 cur = rr;
-                    const uint32_t gc = gcn;
-                    const double lr = lrn;
-                    const int bn = b + T;
-                    if (bn < n) {
-                        rr = vr[bn];
-                        if (paletted) gcn = gcodes[bn >> 2];
-                        else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, bn * 8, 0, 0));
+                auto gather_r = [&](auto dct) {
+                    constexpr bool DC = decltype(dct)::value;
+                    const uint2 *vr = a.vn_rows;
+                    int b = tid;
+                    uint2 rr = make_uint2(0u, 0u);
+                    uint32_t gcn = 0;
+                    double lrn = 0.0;
+                    if (b < n) {
+                        rr = vr[b];
+                        if (paletted) gcn = gcodes[b >> 2];
+                        else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, b * 8, 0, 0));
                     }
-                    const uint32_t cb = codes[b];
-                    codes[b] = 0;
-                    uint32_t rk[4];
-                    double2 ab[4];
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        rk[kk] = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
-                        ab[kk] = rowAB[rk[kk] != 0xFFFFu ? (int)rk[kk] : 0];
+                    for (; b < n; b += T) {
+                        const uint2 cur = rr;
+                        const uint32_t gc = gcn;
+                        const double lr = lrn;
+                        const int bn = b + T;
+                        if (bn < n) {
+                            rr = vr[bn];
+                            if (paletted) gcn = gcodes[bn >> 2];
+                            else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, bn * 8, 0, 0));
+                        }
+                        const uint32_t cb = codes[b];
+                        codes[b] = 0;
+                        uint32_t rk[4];
+                        double2 ab[4];
+    #pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            rk[kk] = ((kk < 2 ? cur.x : cur.y) >> (16 * (kk & 1))) & 0xFFFFu;
+                            ab[kk] = rowAB[rk[kk] != 0xFFFFu ? (int)rk[kk] : 0];
+                        }
+                        double sacc = paletted ? pal[(gc >> ((b & 3) * 2)) & 3u] : lr;
+    #pragma unroll
+                        for (int kk = 0; kk < 4; ++kk) {
+                            const double c = ms_message(ab[kk], (cb >> (2 * kk)) & 1u, ((cb >> (2 * kk)) & 2u) != 0, DC);
+                            sacc = (rk[kk] != 0xFFFFu) ? sacc + c : sacc;
+                        }
+                        total[b] = sacc;
                     }
-                    double sacc = paletted ? pal[(gc >> ((b & 3) * 2)) & 3u] : lr;
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const double c = ms_message(ab[kk], (cb >> (2 * kk)) & 1u, ((cb >> (2 * kk)) & 2u) != 0);
-                        sacc = (rk[kk] != 0xFFFFu) ? sacc + c : sacc;
-                    }
-                    total[b] = sacc;
-                }
+                };
+                if (msclip) gather_r(std::integral_constant<bool, true>{});
+                else gather_r(std::integral_constant<bool, false>{});
                 STAMP(ST_VNK);
                 psync();
                 STAMP(ST_VNK_WAIT);
@@ -608,6 +630,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             const double tlim_it = had_vn ? a.spa_tlim : 1.0;  // tanh(22) = 1
             const bool check = ADAPT ? (it < a.max_it) : (it > 0);
             const bool compute = it < a.max_it;
+            // (iteration 0: b2c unclipped; c2b is +0 there)
+            const double thr_it = had_vn ? thr : __builtin_inf();
             ++epoch;
             int head = head_in, row0 = row0_in;
             uint32_t sm = smask_f;
@@ -618,7 +642,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             // (set only on rows begun in this lane) publishes it.  Slots before
             // the first START are the tail of the previous lane's last row.
             int r = row0;
-            int par = 0, cur_s = 0, mis = 0, neg = 0;
+            int par = 0, cur_s = 0, mis = 0, neg = 0, big = 0;
             int div_unsafe = 0;
             uint32_t zt = 0;  // decisions of the first KT slots (tail parity)
             double acc = 1.0, m1 = DBL_MAX, m2 = DBL_MAX;
@@ -638,16 +662,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
                 } else if constexpr (SPA_FAM) {
-                    double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
-                    if (had_vn) x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
+                    const double x = clip_msg(tv - c2b.get(k), thr_it);  // (:115, :122-123; :21-29)
                     double t = x;
                     if (compute) t = tanh_lin(x / 2.);
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
                 } else {
-                    double x = tv;  // iteration 0: b2c = channel LLR, unclipped (:21-29)
-                    if (had_vn) x = clip_msg(tv - c2b.get(k), thr);  // (:115, :122-123)
+                    const double x = clip_msg(tv - c2b.get(k), thr_it);  // (:115, :122-123; :21-29)
                     c2b.set(k, x);
                     if (k < KT && k > 0) {
                         // the first START closes the tail segment: keep its aggregate
@@ -678,6 +700,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
                     } else {
                         rowAB[r] = ms_pack(m1, m2, cur_s ^ neg, mr);
+                        big |= (m2 > thr) ? 1 : 0;
                     }
                 }
             };
@@ -715,6 +738,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         agg_merge(t, h);
                         const int mr = ppar ^ hpar ^ s_row0;
                         rowAB[row0] = ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr);
+                        big |= (t.m2 > thr) ? 1 : 0;
                         mis |= mr;
                     }
                 }
@@ -723,12 +747,17 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if (mis) __hip_atomic_store(gmis, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 if (mis) *s_flag = epoch;
+                if constexpr (!SPA_FAM) {
+                    if (big) *s_big = epoch;
+                }
             }
             STAMP(ST_CN1);
             psync();
             STAMP(ST_CN1_WAIT);
             const bool anymis = SPLIT ? (__hip_atomic_load(gmis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it + 1)
                                       : (*s_flag == epoch);
+            if constexpr (!SPA_FAM)
+                msclip = a.thr_on && (SPLIT || !had_vn || a.ms_clip_later || *s_big == epoch);
             // SPA: rp / t by div_rn_safe when every t of this wave came out of
             // tanh's common path (|t| in [2^-55, 1]) and every row product of the
             // wave is at least 2^-900 in magnitude: the operand range where the
@@ -761,7 +790,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
                     const double2 ab = rowAB[r];
                     const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
-                    c = ms_message(ab, xneg, eq1);
+                    c = ms_message(ab, xneg, eq1, msclip);
                     if constexpr (VNG_H) {
                         // the two bits at the edge's padded position (dummy slots:
                         // a scratch byte past the last chunk)
