@@ -226,6 +226,38 @@ def test_minsum_bit_gather_and_vn_phases(gpu_available, alg, prim, sec, vng, mon
     assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0, batch=8, llr=llr, synd=s)
 
 
+def _irregular_dv4_code(n=4096, m=900, seed=5):
+    """Random code whose bits have degree 0..4 (isolated bits included) and
+    rows of degree 12..20: the dv <= 4 bit gather with missing terms."""
+    rng = np.random.default_rng(seed)
+    rows = [set() for _ in range(m)]
+    for b in range(n):
+        d = int(rng.choice([0, 1, 2, 3, 4], p=[0.02, 0.08, 0.3, 0.3, 0.3]))
+        for r in rng.choice(m, size=d, replace=False):
+            rows[int(r)].add(b)
+    for r in range(m):  # every row at least 2 edges (a 1-edge row keeps min2 = DBL_MAX)
+        while len(rows[r]) < 2:
+            rows[r].add(int(rng.integers(n)))
+    return Q.HMatrix.from_check_nodes(n, [sorted(r) for r in rows])
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_bit_gather_irregular_low_degree(gpu_available, alg, prim, sec):
+    H = _irregular_dv4_code()
+    g = Q.Graph(H)
+    plan = g.plan(0, alg)
+    assert plan["variant"] == "v2", plan
+    O = Oracle(H)
+    for qber, max_it, thr_on, seed in ((0.03, 50, True, 1), (0.06, 4, True, 2), (0.03, 50, False, 3)):
+        _, _, llr, synd = frames(H, qber, 16, seed)
+        out = g.decode(Q.Params(alg, max_it, thr_on, 100.0, prim, sec), llr, synd, posterior=True)
+        ob, oi, ok, op = O.decode_batch(O.params(alg, max_it, thr_on, 100.0, prim, sec), llr, synd, threads=16,
+                                        posterior=True)
+        for f in range(llr.shape[0]):
+            assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
+            assert bits_equal_nan(out.posterior[f], op[f])
+
+
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
     assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
