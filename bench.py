@@ -38,6 +38,10 @@ WORKLOADS = {
     "c1": ("c1_n1024_m220.alist", 1, 0, 0.0, 0.0, 0.013, 4096, "C1: n=1k R~0.8 SPA 50-iter"),
     "c4": ("c4s_n102400_m32001.alist", 1, 0, 0.0, 0.0, 0.038, 128,
            "C4 stand-in: n=100k R=0.69 SPA 50-iter, batch 128/GPU (R=0.79 file absent upstream)"),
+    # the R=0.79 dv=4 file is absent upstream; a seeded
+    # build-generated code of its shape (qkd_ldpc_v_amd/codes.py), QBER 0.022
+    "c4g": (None, 0, 0, 0.0, 0.0, 0.022, 128,
+            "C4 (ii): generated regular dv=4 n=102400 m=22001 R=0.785 (seed 777) SPA 50-iter, batch 128/GPU"),
     "c5": ("c5_n10240_m2048.sp2", 3, 5, 0.7, 0.99, 0.0156, 4096,
            "C5 decode: n=10k R=0.8 irregular (matrices_2, format 3) AOMSA beta=0.7 sigma=0.99 "
            "(configs/ADAPTIVE T.json, rate bucket 0.805) 50-iter, QBER 1.56%, batch 4096/GPU, no rate adaptation"),
@@ -91,7 +95,10 @@ def main():
 
     fixture, fmt, alg, prim, sec, qber, batch, desc = WORKLOADS[args.workload]
     batch = args.batch or batch
-    H = Q.load_matrix(os.path.join(ROOT, "tests", "golden", "matrices", fixture + ".gz"), fmt)
+    if fixture is None:
+        H = Q.regular_code(102400, 22001, 4, 777)
+    else:
+        H = Q.load_matrix(os.path.join(ROOT, "tests", "golden", "matrices", fixture + ".gz"), fmt)
     n, m, E = H.n, H.m, H.nnz
     k_info = n - m
     g = Q.Graph(H)
@@ -227,10 +234,11 @@ def main():
             "dtype": "f64",
             "data": "synthetic sifted keys from the reference's own trial generator (Xoshiro256++ seeds, "
                     "exactly floor(n*QBER) errors, libstdc++ draw semantics) run on device, untimed; "
-                    "reference parity-check matrix file",
+                    + ("reference parity-check matrix file" if fixture else
+                       "seeded generated parity-check matrix (the reference's file is absent upstream)"),
             "trial_generation_s": trial_gen_s,
             "config": {
-                "workload": desc, "matrix": fixture, "n": n, "m": m, "edges": E, "info_bits_per_frame": k_info,
+                "workload": desc, "matrix": fixture or "generated: regular_code(102400, 22001, 4, 777)", "n": n, "m": m, "edges": E, "info_bits_per_frame": k_info,
                 "algorithm": Q.ALGORITHM_NAMES[alg], "qber": qber, "max_iterations": args.max_iterations,
                 "batch_per_gpu": batch, "global_batch": int(frames_step),
                 "parallelism": f"frames sharded over {world} GPU(s), no collectives",

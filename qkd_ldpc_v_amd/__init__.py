@@ -9,8 +9,10 @@ from ._lib import (ALGORITHM_NAMES, ANMSA, AOMSA, NMSA, OMSA, SPA, SPA_LIN, Para
 from .graph import (DecodeOutput, Graph, HMatrix, RatePlan, adapt_code_rate, keys_match_device, load_matrix,
                     trial_seeds, trials_device, trials_rate_adapt_device, xoshiro_state)
 from .trials import bsc_frames
+from .codes import regular_code
 
 __all__ = [
+    "regular_code",
     "ALGORITHM_NAMES", "ANMSA", "AOMSA", "NMSA", "OMSA", "SPA", "SPA_LIN", "Params", "QLDPCError",
     "exported_symbols", "lib", "log_p", "version", "DecodeOutput", "Graph", "HMatrix", "keys_match_device",
     "trial_seeds", "trials_device", "RatePlan", "adapt_code_rate", "trials_rate_adapt_device", "xoshiro_state",

@@ -346,7 +346,7 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
 
 // V2 split plan, for codes whose frame does not fit one CU (totals beyond LDS
 // or more edges than 16 waves x 64 lanes x 40 slots): K parts of 16 waves
-// each (one workgroup per part, K <= 8 so a part group fits well inside one
+// each (one workgroup per part, K <= 16 so a part group fits well inside one
 // XCD's 32 CUs), rows dealt to the 16K waves as in plan_v2 (contiguous
 // balanced blocks), part r = waves [16r, 16r + 16).  Totals go to global
 // memory.  QLDPC_SPLIT=0 disables it (v1 is used).
@@ -362,7 +362,9 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr) {
     const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
     if (kforce && (kforce < kmin || kforce > 32)) return false;
-    for (int K = kforce ? kforce : kmin; K <= (kforce ? kforce : 8); ++K) {
+    // (K need not divide an XCD's 32 workgroups: groups form in claim order and
+    // a workgroup joins the next group whenever it finishes a frame)
+    for (int K = kforce ? kforce : kmin; K <= (kforce ? kforce : 16); ++K) {
         const int W = WP * K;
         const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
         if (cap > 64LL * R) continue;

@@ -289,6 +289,24 @@ def test_c4_100k_split_full_decode(gpu_available):
     assert out.iterations.min() < 50
 
 
+@pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
+def test_c4_generated_dv4_ten_parts(gpu_available, alg, prim, sec):
+    """the generated n=102400 dv=4 code needs more than
+    8 parts per frame (409,600 edges; the planner picks 11), a count that does
+    not divide an XCD's 32 workgroups."""
+    H = Q.regular_code(102400, 22001, 4, 777)
+    g = Q.Graph(H)
+    plan = g.plan(0, alg)
+    assert plan["variant"] == "v2_split" and plan["lanes"] >= 10 * 1024 and plan["lanes"] % 1024 == 0, plan
+    O = Oracle(H)
+    _, _, llr, synd = frames(H, 0.022, 6, 4242)
+    out = g.decode(Q.Params(alg, 50, True, 100.0, prim, sec), llr, synd, posterior=True)
+    ob, oi, ok, op = O.decode_batch(O.params(alg, 50, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
+    for f in range(llr.shape[0]):
+        assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
+        assert bits_equal_nan(out.posterior[f], op[f])
+
+
 @pytest.mark.parametrize("batch", [1, 2])
 def test_c4_100k_split_few_frames(gpu_available, batch):
     # fewer frames than XCDs: most part groups draw no frame and leave

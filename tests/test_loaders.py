@@ -97,3 +97,22 @@ def test_host_mirror_program_loads(tmp_path):
     assert r.returncode == 0 and r.stdout.split() == ["10240", "2201", "40960", "0"]
     r = subprocess.run([exe, "load", "/nonexistent", "1"], capture_output=True, text=True)
     assert r.returncode == 1 and "ERROR: Failed to open file" in r.stdout
+
+
+def test_generated_regular_code():
+    """codes.regular_code (the C4 (ii) stand-in): exact degrees, distinct rows
+    per bit, ascending adjacency, deterministic per seed."""
+    import numpy as np
+    import qkd_ldpc_v_amd as Q
+
+    H = Q.regular_code(4000, 861, 4, 777)
+    assert (H.n, H.m, H.nnz) == (4000, 861, 16000)
+    assert set(np.diff(H.col_ptr)) == {4}
+    dc = np.diff(H.row_ptr)
+    assert dc.max() - dc.min() <= 1
+    for j in range(H.m):
+        r = H.col_idx[H.row_ptr[j]:H.row_ptr[j + 1]]
+        assert (np.diff(r) > 0).all()
+    H2 = Q.regular_code(4000, 861, 4, 777)
+    assert np.array_equal(H.col_idx, H2.col_idx)
+    assert not np.array_equal(H.col_idx, Q.regular_code(4000, 861, 4, 778).col_idx)
