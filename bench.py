@@ -55,6 +55,23 @@ WORKLOADS = {
 SIMULATION_SEEDS = {"c1": 9012025, "c2": 1022025, "c3": 10022025}
 RATE_ADAPT = {"c5ra": (0.06, 1.39, "c5_n10240_m2048.untp")}  # delta, efficiency, untainted list
 
+# The C5 sweep: configs/ADAPTIVE T.json's 26 (code rate,
+# QBER, delta, f_EC) points (:102-130) with AOMSA beta / sigma per code rate
+# (:51-76) and the format-3 matrices of sparse_matrices/matrices_2.
+C5_MATRIX = {0.805: "c5_n10240_m2048", 0.655: "c5b_n10240_m3584", 0.505: "c5c_n10240_m5120"}
+C5_BETA_SIGMA = {0.805: (0.7, 0.99), 0.655: (0.74, 0.94), 0.505: (0.72, 0.85)}
+C5_POINTS = [
+    (0.805, 0.0076, 0.10, 1.85), (0.805, 0.0116, 0.09, 1.50), (0.805, 0.0156, 0.06, 1.39),
+    (0.805, 0.0196, 0.03, 1.28), (0.805, 0.0236, 0.01, 1.21), (0.805, 0.0276, 0.11, 1.20),
+    (0.805, 0.0316, 0.22, 1.22), (0.655, 0.0368, 0.12, 1.22), (0.655, 0.0408, 0.10, 1.20),
+    (0.655, 0.0448, 0.06, 1.18), (0.655, 0.0488, 0.06, 1.17), (0.655, 0.0528, 0.01, 1.16),
+    (0.655, 0.0568, 0.06, 1.16), (0.655, 0.0608, 0.11, 1.17), (0.655, 0.0648, 0.16, 1.17),
+    (0.655, 0.0688, 0.23, 1.19), (0.505, 0.0734, 0.12, 1.18), (0.505, 0.0774, 0.09, 1.17),
+    (0.505, 0.0814, 0.08, 1.16), (0.505, 0.0854, 0.04, 1.15), (0.505, 0.0894, 0.01, 1.14),
+    (0.505, 0.0934, 0.03, 1.14), (0.505, 0.0974, 0.06, 1.14), (0.505, 0.1014, 0.10, 1.15),
+    (0.505, 0.1054, 0.13, 1.16), (0.505, 0.1094, 0.13, 1.15),
+]
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -76,6 +93,8 @@ def main():
                          "--streams > 1 a timed step's decode shares CUs with its neighbours)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c5-point", type=int, default=-1,
+                    help="with --workload c5ra: one of the 26 C5 sweep points (C5_POINTS index)")
     args = ap.parse_args()
 
     import torch
@@ -95,6 +114,16 @@ def main():
 
     fixture, fmt, alg, prim, sec, qber, batch, desc = WORKLOADS[args.workload]
     batch = args.batch or batch
+    ra = RATE_ADAPT.get(args.workload)
+    if args.c5_point >= 0:
+        if args.workload != "c5ra":
+            raise SystemExit("--c5-point needs --workload c5ra")
+        crate, qber, delta, eff = C5_POINTS[args.c5_point]
+        fixture = C5_MATRIX[crate] + ".sp2"
+        prim, sec = C5_BETA_SIGMA[crate]
+        ra = (delta, eff, C5_MATRIX[crate] + ".untp")
+        desc = (f"C5 sweep point {args.c5_point}: code rate {crate} ({fixture}), QBER {qber}, delta {delta}, "
+                f"f_EC {eff}, AOMSA beta={prim} sigma={sec} 50-iter, batch {batch}/GPU (configs/ADAPTIVE T.json)")
     if fixture is None:
         H = Q.regular_code(102400, 22001, 4, 777)
     else:
@@ -109,12 +138,11 @@ def main():
     # The reference's generator (src/simulation.cpp:540-551,713-719,743):
     # per-trial seeds drawn from Xoshiro256++(SIMULATION_SEED); each rank takes
     # its own contiguous slice of trials.
-    sim_seed = SIMULATION_SEEDS.get(args.workload, 1022025)
+    sim_seed = 5555 if args.c5_point >= 0 else SIMULATION_SEEDS.get(args.workload, 1022025)  # ADAPTIVE T.json:5
     seeds = Q.trial_seeds(sim_seed, batch * world)[rank * batch:(rank + 1) * batch]
     d_seeds = torch.from_numpy(seeds.view(np.int64)).to(dev)
     ta = torch.empty((batch, n), dtype=torch.uint8, device=dev)
     tb = torch.empty((batch, n), dtype=torch.uint8, device=dev)
-    ra = RATE_ADAPT.get(args.workload)
     if ra:  # adapt_code_rate on the host, then the rate-adapted trials
         import gzip
 

@@ -451,7 +451,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
     }
     for (int i = 0; i < n; ++i) g->dv_max = std::max(g->dv_max, dv[i]);
-    if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 64");
+    if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 511");
     // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
     const char *want = std::getenv("QLDPC_VARIANT");
     const bool v1_only = want && std::strcmp(want, "v1") == 0;
@@ -487,9 +487,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // V2 metadata differs in three ways: the END of a lane's tail (a row begun
     // in the lane before) is cleared — the kernel finishes split rows after a
     // shuffle; slots past the lane's edges up to the group count are dummy
-    // edges (column n, kpos 63, no flags), so every lane of a wave runs the
-    // same slots; lanes count the rows they start (lane_nst).
-    const uint32_t DUMMY = (uint32_t)n | (63u << META_KPOS_SHIFT);
+    // edges (column n, kpos META_KPOS_MASK, no flags), so every lane of a wave
+    // runs the same slots; lanes count the rows they start (lane_nst).
+    const uint32_t DUMMY = (uint32_t)n | (META_KPOS_MASK << META_KPOS_SHIFT);
     const int W = v2 ? T / 64 : 1;
     // V2 min-sum metadata lists each row's edges by kpos: the min-sum row
     // aggregate and parity are order-free, and grouping a

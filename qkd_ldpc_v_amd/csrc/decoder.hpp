@@ -8,11 +8,11 @@ namespace qldpc {
 // Per-slot metadata word (slot-major [slot][lane], one uint32 per CSR edge).
 constexpr uint32_t META_COL_MASK = 0xFFFFFu;   // bit id (n <= 2^20)
 constexpr int META_KPOS_SHIFT = 20;            // position of the edge in its bit's check list
-constexpr uint32_t META_KPOS_MASK = 0x3Fu;     // dv <= 64
-constexpr uint32_t META_START = 1u << 26;      // first edge of its row
-constexpr uint32_t META_END = 1u << 27;        // last edge of its row
-constexpr uint32_t META_VALID = 1u << 28;      // slot holds an edge (tail padding otherwise)
-constexpr int MAX_DV = 64;
+constexpr uint32_t META_KPOS_MASK = 0x1FFu;    // dv < 511 (511 marks a V2 dummy slot)
+constexpr uint32_t META_START = 1u << 29;      // first edge of its row
+constexpr uint32_t META_END = 1u << 30;        // last edge of its row
+constexpr uint32_t META_VALID = 1u << 31;      // slot holds an edge (tail padding otherwise)
+constexpr int MAX_DV = (int)META_KPOS_MASK;
 constexpr int MAX_N = 1 << 20;
 
 // Registers available for per-edge messages in the register-resident variant.

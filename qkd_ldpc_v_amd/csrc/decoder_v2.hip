@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
             }
             if constexpr (GATHER) {
-                if (kp >= (uint32_t)k0 && kp != 63u) {
+                if (kp >= (uint32_t)k0 && kp != META_KPOS_MASK) {
                     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, c), stage_rs, (int)(mt2 * 8),
                                                           0, 0);
@@ -800,7 +800,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     } else if constexpr (VNG) {
                         // record the two bits the bit gather rebuilds this message from
                         const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-                        if (kp < 4u) {  // (dummy slots: kpos 63)
+                        if (kp < 4u) {  // (dummy slots: kpos META_KPOS_MASK)
                             const int col = (int)(mt & META_COL_MASK);
                             __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes) + (col >> 2),
                                                   (xneg | (eq1 ? 2u : 0u)) << (((col & 3) << 3) + 2 * kp),

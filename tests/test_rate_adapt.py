@@ -98,3 +98,65 @@ def test_rate_adapted_pipeline_bitexact(gpu_available, alg, prim, sec):
         assert np.array_equal(it.cpu().numpy().astype(np.uint32), oi)
         assert np.array_equal(ok.cpu().numpy(), ook)
         assert np.array_equal(km.cpu().numpy(), (ob == oa).all(axis=1).astype(np.uint8))
+
+
+# The other two code rates of the sweep (configs/ADAPTIVE T.json maps for the
+# 0.655 and 0.505 buckets; AOMSA beta / sigma of those buckets)
+OTHER_RATES = [
+    ("c5b_n10240_m3584", 0.74, 0.94, [(0.0408, 0.1, 1.2), (0.0528, 0.01, 1.16), (0.0688, 0.23, 1.19)]),
+    ("c5c_n10240_m5120", 0.72, 0.85, [(0.0774, 0.09, 1.17), (0.0894, 0.01, 1.14), (0.1094, 0.13, 1.15)]),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,beta,sigma,points", OTHER_RATES)
+def test_rate_adapted_other_code_rates(gpu_available, name, beta, sigma, points):
+    """R=0.65 and R=0.5 format-3 matrices: rate-adapted AOMSA frames built on
+    device and decoded, bit-exact against the oracle (posteriors included)."""
+    import torch
+
+    H = load_fixture(name + ".sp2")
+    u = np.array(gzip.open(matrix_path(name + ".untp")).read().split(), np.int32)
+    g = Q.Graph(H)
+    O = Oracle(H)
+    st = Q.xoshiro_state(5555)
+    batch = 12
+    seeds = Q.trial_seeds(5555, batch)
+    dev = torch.device("cuda:0")
+    done = 0
+    for q, d, e in points:
+        pp, sp, _ = Q.adapt_code_rate(H.n, H.m, q, d, e, u, st)
+        if pp.size + sp.size == 0:
+            continue
+        done += 1
+        plan = g.rate_plan(pp, sp)
+        ds = torch.from_numpy(seeds.view(np.int64)).to(dev)
+        ta = torch.empty((batch, H.n), dtype=torch.uint8, device=dev)
+        tb = torch.empty_like(ta)
+        pa = torch.empty((batch, max(1, pp.size)), dtype=torch.uint8, device=dev)
+        pb = torch.empty_like(pa)
+        qa = Q.trials_rate_adapt_device(H.n, q, ds, pp.size, ta, tb, pa, pb)
+        lp = torch.full((batch,), Q.log_p(qa), dtype=torch.float64, device=dev)
+        ax = torch.empty_like(ta)
+        llr = torch.empty((batch, H.n), dtype=torch.float64, device=dev)
+        syn = torch.empty((batch, H.m), dtype=torch.uint8, device=dev)
+        bits = torch.empty_like(ta)
+        it = torch.empty(batch, dtype=torch.int32, device=dev)
+        ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+        km = torch.empty(batch, dtype=torch.uint8, device=dev)
+        par = Q.Params(Q.AOMSA, 50, True, 100.0, beta, sigma)
+        g.qkd_ldpc_rate_adapt_device(plan, par, ta, tb, pa, pb, lp, ax, llr, syn, bits, it, ok, km)
+        torch.cuda.synchronize()
+        oa, ol = zip(*[P.trial_rate_adapt(H.n, q, int(sd), pp, sp)[:2] for sd in seeds])
+        oa, ol = np.stack(oa), np.stack(ol)
+        assert np.array_equal(ax.cpu().numpy(), oa)
+        osyn = H.syndrome(oa)
+        assert np.array_equal(syn.cpu().numpy(), osyn)
+        ob, oi, ook, op = O.decode_batch(O.params(Q.AOMSA, 50, True, 100.0, beta, sigma), ol, osyn, threads=8,
+                                         posterior=True)
+        assert np.array_equal(bits.cpu().numpy(), ob)
+        assert np.array_equal(it.cpu().numpy().astype(np.uint32), oi)
+        assert np.array_equal(ok.cpu().numpy(), ook)
+        out = g.decode(par, llr.cpu().numpy(), osyn, posterior=True)
+        assert bits_equal_nan(out.posterior, op)
+    assert done >= 2

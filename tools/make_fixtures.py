@@ -28,6 +28,10 @@ FIXTURES = {
                                  "C4 stand-in: 100k R=0.69 (the R=0.79 file is absent upstream)"),
     "c5_n10240_m2048.sp2": ("matrices_2/(N=10240,M=2048,R=0.8).mtrx", 3, "C5: format-3 irregular R=0.8"),
     "c5_n10240_m2048.untp": ("matrices_2/(N=10240,M=2048,R=0.8).untp", -1, "C5 untainted puncturing cache"),
+    "c5b_n10240_m3584.sp2": ("matrices_2/(N=10240,M=3584,R=0.65).mtrx", 3, "C5 sweep: format-3 irregular R=0.65"),
+    "c5b_n10240_m3584.untp": ("matrices_2/(N=10240,M=3584,R=0.65).untp", -1, "C5 sweep: R=0.65 untainted list"),
+    "c5c_n10240_m5120.sp2": ("matrices_2/(N=10240,M=5120,R=0.5).mtrx", 3, "C5 sweep: format-3 irregular R=0.5"),
+    "c5c_n10240_m5120.untp": ("matrices_2/(N=10240,M=5120,R=0.5).untp", -1, "C5 sweep: R=0.5 untainted list"),
     "kat_n6_m4.dense": ("matrices_uncompressed/(N=6,K=2,M=4,R=0.34).mtrx", 0, "Johnson Ex. 2.5 KAT matrix"),
     "u_n7_m3.dense": ("matrices_uncompressed/(N=7,K=4,M=3,R=0.57).mtrx", 0, "small uncompressed"),
     "u_n10_m5.dense": ("matrices_uncompressed/(N=10,K=5,M=5,R=0.5).mtrx", 0, "small uncompressed"),
