@@ -55,8 +55,8 @@ struct V2Layout {
         total = o; o = split ? o : al16(o + (size_t)(n + 1) * 8);
         rows = o; o = al16(o + (size_t)m * (minsum ? 16 : 8));  // SPA: product; min-sum: {min1, min2}
         rowflag = o;  // (min-sum row flags ride in the sign bits of rowAB: none here)
-        tail = o; o = al16(o + (minsum ? (size_t)T * 16 : 0));    // min-sum: a lane's tail aggregate
-        tailneg = o; o = al16(o + (minsum ? (size_t)T * 4 : 0));
+        tail = o;     // (min-sum: a lane's tail aggregate is parked in its row's rowAB entry)
+        tailneg = o;
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         bytes = o;
@@ -150,8 +150,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     double *rowA = rowA_lds;
     double2 *rowAB = rowAB_lds;
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
-    double2 *tailagg = reinterpret_cast<double2 *>(smem + L.tail);
-    int *tailneg = reinterpret_cast<int *>(smem + L.tailneg);
     uint8_t *codes = smem + V2_CODES_OFF;
 
     EdgeMsgsH<R, RG, RL> c2b;
@@ -672,11 +670,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const double x = clip_msg(tv - c2b.get(k), thr_it);  // (:115, :122-123; :21-29)
                     c2b.set(k, x);
                     if (k < KT && k > 0) {
-                        // the first START closes the tail segment: keep its aggregate
-                        if (k == head) {
-                            tailagg[tid] = make_double2(m1, m2);
-                            tailneg[tid] = neg;
-                        }
+                        // the first START closes the tail segment: park its aggregate
+                        // (parity of negatives in min1's sign bit) in the split row's
+                        // own entry, which nothing else touches until the merge below
+                        if (k == head) rowAB[row0] = ms_pack(m1, m2, neg, 0);
                     }
                     m1 = start ? DBL_MAX : m1;
                     m2 = start ? DBL_MAX : m2;
@@ -730,11 +727,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     t.m2 = __shfl(m2, up, 64);
                     t.neg = __shfl(neg, up, 64);
                     if (head > 0) {
-                        const double2 ta = tailagg[tid];
+                        const double2 ta = rowAB[row0];
                         MinAgg h;
-                        h.m1 = ta.x;
+                        h.m1 = __builtin_fabs(ta.x);
                         h.m2 = ta.y;
-                        h.neg = tailneg[tid];
+                        h.neg = (int)(ql_exact::hi_word(ta.x) >> 31);
                         agg_merge(t, h);
                         const int mr = ppar ^ hpar ^ s_row0;
                         rowAB[row0] = ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr);
