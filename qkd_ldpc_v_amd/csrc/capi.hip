@@ -145,6 +145,8 @@ struct Xoshiro256pp {
 struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
     bool vng = false;                       // V2 min-sum bit gather tables built
+    bool vng_h_fit = false;                 // hybrid bit gather's padded edge codes fit LDS (set before planning)
+    bool rows_global_ms = false;            // hybrid min-sum: row aggregates in global scratch
     int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
     std::vector<int> wave_rows;             // V2: first layout row of each wave (+ m)
     std::vector<int> row_order;             // V2: layout row -> original row
@@ -174,7 +176,8 @@ int block_threads(const qldpc_graph &g) {
 
 size_t lds_of(const qldpc_graph &g, int alg) {
     if (g.variant == VAR_V2 && g.split_k > 1) return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true);
-    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG) : lds_bytes_for(g.variant, g.n, g.m, g.T);
+    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG, g.rows_global_ms && alg >= 2)
+                               : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
 int env_int(const char *name, int dflt) {
@@ -303,7 +306,17 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         int W = forced > 0 ? forced : (int)std::min<long long>(wmax, (E + 64LL * g.max_dc - 1) / (64LL * g.max_dc));
         W = std::max(1, W);
         if (W > wmax) continue;
-        if (lds_bytes_v2(2, g.n, g.m, W * 64) > LDS_LIMIT) continue;
+        // min-sum row aggregates (16 B/row) must fit beside the totals; on the
+        // hybrid shape they may live in global scratch instead when the bit
+        // gather applies (then only the SPA image, 8 B/row, must fit)
+        bool rows_global = false;
+        if (lds_bytes_v2(2, g.n, g.m, W * 64) > LDS_LIMIT) {
+            if (sh[1] == 0 || !g.vng_h_fit || g.m >= 0xFFFF ||
+                lds_bytes_v2(0, g.n, g.m, W * 64, false, sh[0], sh[1]) > LDS_LIMIT ||
+                lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], true) > LDS_LIMIT)
+                continue;
+            rows_global = true;
+        }
         const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
         std::vector<long long> sums;
         const auto waves = balance_rows(row_ptr, g.m, W, cap, sums);
@@ -334,6 +347,7 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         g.variant = VAR_V2;
         g.v2R = sh[0];
         g.v2RG = sh[1];
+        g.rows_global_ms = rows_global;
         g.T = W * 64;
         g.EPL = epl;
         g.wave_rows = rb;
@@ -451,6 +465,11 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
     }
     for (int i = 0; i < n; ++i) g->dv_max = std::max(g->dv_max, dv[i]);
+    {
+        long long chunks = 0;
+        for (int i = 0; i < n; ++i) chunks += (dv[i] + 3) / 4;
+        g->vng_h_fit = chunks + V2_VNG_DUMMY_CHUNKS <= V2_CODES_CAP && g->dv_max < 256;
+    }
     if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 511");
     // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
     const char *want = std::getenv("QLDPC_VARIANT");
@@ -730,9 +749,16 @@ int check_params(const qldpc_params *p) {
 }
 
 // Per-workgroup scratch of the V2 kernels: overflow message slots, then the VN stage.
+// Hybrid min-sum with rows in global scratch: their offset (16-byte aligned).
+long long v2_rows_offset(const qldpc_graph &g) {
+    return ((long long)g.v2RG * REG_TSTRIDE + g.stage_doubles + 1) / 2 * 2;
+}
+
 long long v2_scratch_doubles(const qldpc_graph &g) {
     if (g.split_k > 1) return 32;  // the stage is per frame (Workspace::gstage)
-    return ((long long)g.v2RG * REG_TSTRIDE + g.stage_doubles + 31) / 32 * 32;
+    const long long end = g.rows_global_ms ? v2_rows_offset(g) + 2LL * g.m
+                                           : (long long)g.v2RG * REG_TSTRIDE + g.stage_doubles;
+    return (end + 31) / 32 * 32;
 }
 
 // Per-stream workspace of a device graph, created on first use.
@@ -853,6 +879,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.vn_k0 = g->vn_k0; a.n_hd = g->n_hd; a.hd_bits = dg->hd_bits; a.hd_dv = dg->hd_dv; a.stage_off = dg->stage_off;
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
+    a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
     a.row_orig = dg->row_orig;
     a.split_k = v2 ? g->split_k : 1;
     if (v2 && g->split_k > 1) {
@@ -883,6 +910,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
                 a.slot_meta2 = dg->vng_meta2;
             }
         }
+        if (a.rows_wg_offset >= 0 && !a.vn_rows)
+            return fail(QLDPC_EUNSUP, "this code's min-sum row aggregates need the bit gather (QLDPC_VNG=0 given)");
     }
     if (v2 && !codes_ready)
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));

@@ -124,6 +124,10 @@ struct DecodeArgs {
     // Min-sum: the factor/offset can push |message| above its selected
     // minimum (|NMSA factor| > 1, negative offset, or NaN): clip every message.
     int ms_clip_later;
+    // Hybrid min-sum whose row aggregates do not fit LDS beside the totals
+    // (C5 R=0.5: m = 5120): rowAB lives in the workgroup's global scratch
+    // (L2-resident) at this offset in doubles; -1: rows in LDS.
+    long long rows_wg_offset;
 };
 
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
@@ -142,7 +146,8 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                hipStream_t stream);
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0);
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0,
+                    bool rows_global = false);
 // Whether a V2 shape can run the min-sum bit gather (DecodeArgs::vn_rows):
 // the dv <= 4 register shape, or the hybrid shape when the padded edge
 // positions' two code bits fit the LDS byte area.

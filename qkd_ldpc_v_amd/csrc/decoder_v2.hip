@@ -75,10 +75,10 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 // SPLIT: a frame is decoded by a.split_k workgroups of one XCD (planner
 // parts: contiguous blocks of 16 waves' rows), which meet at every phase
 // boundary through a global arrival counter; totals are in global memory.
-template <bool SPLIT, int RL>
+template <bool SPLIT, int RL, bool RGLB>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true);
-    else return V2Layout(a.n, a.m, a.nc, a.T, minsum, false, RL);
+    else return V2Layout(a.n, RGLB ? 0 : a.m, a.nc, a.T, minsum, false, RL);
 }
 
 // Whether a launch runs the LDS-slot instantiation (RL = V2_RL): SPA family,
@@ -117,7 +117,9 @@ __device__ __forceinline__ void group_sync(int *ctr, int target, int *err) {
 // after one barrier each thread rebuilds a bit's messages from its rows'
 // aggregates — the same operations the message pass ran — and sums them in
 // kpos order onto the channel LLR (std::accumulate order, :78).
-template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false>
+// RGLB (hybrid min-sum bit gather only): the row aggregates live in the
+// workgroup's global scratch instead of LDS (a.rows_wg_offset).
+template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false, bool RGLB = false>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
@@ -140,7 +142,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // threshold_matrix disabled == clipping at +inf (|v| > inf never holds; NaN passes)
     const double thr = a.thr_on ? a.thr : __builtin_inf();
     const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
-    const V2Layout L = v2_layout<SPLIT, RL>(a, !SPA_FAM);
+    static_assert(!RGLB || (VNG && RG > 0), "rows in global scratch: hybrid bit gather only");
+    const V2Layout L = v2_layout<SPLIT, RL, RGLB>(a, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
     int *s_part = reinterpret_cast<int *>(smem) + 2;  // SPLIT: rank, sync slot
@@ -149,6 +152,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     double2 *const rowAB_lds = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
     double *rowA = rowA_lds;
     double2 *rowAB = rowAB_lds;
+    if constexpr (RGLB)
+        rowAB = reinterpret_cast<double2 *>(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.rows_wg_offset);
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
     uint8_t *codes = smem + V2_CODES_OFF;
 
@@ -913,7 +918,15 @@ KernelFn pick_v2(int alg) {
     }
 }
 
-KernelFn kernel_v2_vng(int alg, int RG) {
+KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
+    if (RG > 0 && rglb) {
+        switch (alg) {
+        case 2: return decode_v2_kernel<2, V2_R_SMALL, V2_RG_HYBRID, false, 0, true, true>;
+        case 3: return decode_v2_kernel<3, V2_R_SMALL, V2_RG_HYBRID, false, 0, true, true>;
+        case 4: return decode_v2_kernel<4, V2_R_SMALL, V2_RG_HYBRID, false, 0, true, true>;
+        default: return decode_v2_kernel<5, V2_R_SMALL, V2_RG_HYBRID, false, 0, true, true>;
+        }
+    }
     if (RG > 0) {
         switch (alg) {
         case 2: return decode_v2_kernel<2, V2_R_SMALL, V2_RG_HYBRID, false, 0, true>;
@@ -941,9 +954,9 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG) {
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, bool rows_global) {
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
-    return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0).bytes;
+    return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0).bytes;
 }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
@@ -954,7 +967,8 @@ bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
-    KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG)
+    if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
+    KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
                                        v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),

@@ -259,6 +259,16 @@ def test_bit_gather_irregular_low_degree(gpu_available, alg, prim, sec):
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
+@pytest.mark.parametrize("name,qber", [("c5b_n10240_m3584.sp2", 0.045), ("c5c_n10240_m5120.sp2", 0.085)])
+def test_c5_other_code_rates_all_algorithms(gpu_available, name, qber, alg, prim, sec):
+    """R=0.65 (m=3584) and R=0.5 (m=5120, a bit of degree 66) format-3 codes on
+    the hybrid shape; R=0.5's min-sum row aggregates live in global scratch."""
+    assert graph(name).plan(0, alg)["variant"] == "v2_hybrid"
+    assert_parity(name, alg, prim, sec, qber=qber, batch=8, seed=60 + alg)
+    assert_parity(name, alg, prim, sec, qber=qber, batch=4, seed=70 + alg, max_it=2, thr_on=False)
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
     assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
     assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.025, batch=12, seed=50 + alg)
