@@ -152,6 +152,7 @@ struct qldpc_graph {
     std::vector<int> row_order;             // V2: layout row -> original row
     std::vector<int> layout_row_ptr;        // V2: row_ptr of the rows in layout order
     int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
+    int hd_uniform_dv = 0;                  // > 0: the staged bits are 0..n-1 in order, all of this degree
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
     std::vector<int> part_row0;             // V2 split: first layout row of each part (+ m)
@@ -553,6 +554,11 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         g->stage_doubles = off;
     }
     g->n_hd = (int)hd_bits.size();
+    if (g->n_hd == n && n > 0) {
+        bool uni = true;
+        for (int i = 0; i < n && uni; ++i) uni = hd_bits[i] == i && hd_dv[i] == hd_dv[0];
+        g->hd_uniform_dv = (uni && env_int("QLDPC_HD_TABLES", 0) == 0) ? hd_dv[0] : 0;  // (env: A/B)
+    }
     const int S4 = G4 * 4;  // V2 slots per lane (register + scratch)
     // Min-sum bit gather (VNG).  Register shape, dv <= 4: per bit, the layout
     // rows of its kpos-th edge (u16 each, 0xFFFF past its degree).  Hybrid
@@ -876,6 +882,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.frame_counter = w->counter;
     a.scratch = w->scratch;
     a.scratch_wg_doubles = v2 ? v2_scratch_doubles(*g) : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.hd_uniform_dv = g->hd_uniform_dv;
     a.vn_k0 = g->vn_k0; a.n_hd = g->n_hd; a.hd_bits = dg->hd_bits; a.hd_dv = dg->hd_dv; a.stage_off = dg->stage_off;
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;

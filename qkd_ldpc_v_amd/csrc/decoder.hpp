@@ -95,6 +95,7 @@ struct DecodeArgs {
     int n_hd;                       // bits with degree > vn_k0
     const int32_t *hd_bits;         // [n_hd]
     const int32_t *hd_dv;           // [n_hd]
+    int hd_uniform_dv;              // > 0: hd_bits[i] == i and hd_dv[i] == this for every i
     const int32_t *stage_off;       // [dv_max]: offset of term kk's block in the stage
     const uint32_t *slot_meta2;     // like slot_meta: stage index of the slot's edge
     long long stage_wg_offset;      // doubles from a workgroup's scratch base to its stage

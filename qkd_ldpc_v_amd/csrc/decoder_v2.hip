@@ -543,11 +543,20 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     // four bits per lane at a time: their stage loads overlap
                     for (int i0 = h0 + tid; i0 < h1; i0 += 4 * T) {
                         int b[4], dvb[4];
+                        if (a.hd_uniform_dv > 0) {  // regular code, bits in id order: no table loads
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int i = i0 + j * T;
-                            b[j] = (i < h1) ? a.hd_bits[i] : -1;
-                            dvb[j] = (i < h1) ? a.hd_dv[i] : 0;
+                            for (int j = 0; j < 4; ++j) {
+                                const int i = i0 + j * T;
+                                b[j] = (i < h1) ? i : -1;
+                                dvb[j] = (i < h1) ? a.hd_uniform_dv : 0;
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int i = i0 + j * T;
+                                b[j] = (i < h1) ? a.hd_bits[i] : -1;
+                                dvb[j] = (i < h1) ? a.hd_dv[i] : 0;
+                            }
                         }
                         double sacc[4];
 #pragma unroll
