@@ -391,7 +391,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const double d = sel - fac;
                 c = prod * ((d < 0.) ? 0. : d);
             }
-            if (doclip) c = clip_msg(c, thr);  // (:73-74; a no-op otherwise, see msclip)
+            if (doclip) {  // (:73-74; a no-op otherwise, see msclip)
+                // a real scalar branch on the uniform flag: the empty volatile
+                // asm keeps the compiler from turning the clip into selects
+                asm volatile("");
+                c = clip_msg(c, thr);
+            }
             return c;
         };
         // Message emission shared by both message passes: c2b, VN phase 0
