@@ -20,13 +20,16 @@ $(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/
 $(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/order.o: $(CSRC)/order.hip $(CSRC)/decoder.hpp
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/loaders.o: $(CSRC)/loaders.cpp $(CSRC)/loaders.hpp
 	g++ -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(LIB): $(CSRC)/decoder.o $(CSRC)/decoder_v2.o $(CSRC)/trials.o $(CSRC)/capi.o $(CSRC)/loaders.o
+$(LIB): $(CSRC)/decoder.o $(CSRC)/decoder_v2.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi.o $(CSRC)/loaders.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
 # Diagnostic build with per-phase s_memtime stamps (never the product).
@@ -38,7 +41,7 @@ $(CSRC)/decoder_v2_st.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSR
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
-$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
+$(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi_st.o $(CSRC)/loaders.o
 	mkdir -p $(PKG)/diag
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -lz -o $@
 
@@ -65,5 +68,5 @@ AB ?= x
 ab:
 	mkdir -p $(PKG)/ab/$(AB)
 	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/decoder_v2.hip -o $(PKG)/ab/$(AB)/decoder_v2.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/capi.o $(CSRC)/loaders.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi.o $(CSRC)/loaders.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
 .PHONY: ab

@@ -63,6 +63,9 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     int *split_ctl = nullptr;
     double *gtotal = nullptr, *gstage = nullptr;
     size_t split_frames = 0;
+    // frame claim order (order.hip): per-frame weights and the sorted order
+    int32_t *fweight = nullptr, *forder = nullptr;
+    size_t order_frames = 0;
 };
 
 struct HostIO {  // device staging buffers of the host-buffer entry
@@ -89,8 +92,9 @@ struct DeviceGraph {
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
     uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
-    std::mutex mu;
+    std::mutex mu;     // workspaces (ws), occupancy cache
     std::map<void *, Workspace> ws;
+    std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
     HostIO io;
     int occ[6] = {0, 0, 0, 0, 0, 0};
 };
@@ -790,10 +794,14 @@ int ensure_codes(qldpc_graph *g, Workspace *w, int batch, hipStream_t stream) {
 // out waiting for its members (the kernel never hangs on it; results are void).
 int split_check(qldpc_graph *g, DeviceGraph *dg, hipStream_t stream) {
     if (g->variant != VAR_V2 || g->split_k <= 1) return QLDPC_OK;
-    Workspace *w = workspace(dg, stream);
-    if (!w->split_ctl) return QLDPC_OK;
+    int *ctl = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(dg->mu);  // ws is shared with other streams' calls
+        ctl = workspace(dg, stream)->split_ctl;
+    }
+    if (!ctl) return QLDPC_OK;
     int err = 0;
-    HIP_TRY(hipMemcpy(&err, w->split_ctl + 16, sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&err, ctl + 16, sizeof(int), hipMemcpyDeviceToHost));
     if (err) return fail(QLDPC_EHIP, "split frame: a part group failed to meet (results void)");
     return QLDPC_OK;
 }
@@ -842,6 +850,15 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
                 HIP_TRY(hipMalloc(&w->gstage, (size_t)batch * std::max<long long>(1, g->stage_doubles) * sizeof(double)));
                 w->split_frames = (size_t)batch;
             }
+        }
+        if ((size_t)batch > w->order_frames) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            (void)hipFree(w->fweight);
+            (void)hipFree(w->forder);
+            w->fweight = nullptr; w->forder = nullptr; w->order_frames = 0;
+            HIP_TRY(hipMalloc(&w->fweight, (size_t)batch * sizeof(int32_t)));
+            HIP_TRY(hipMalloc(&w->forder, (size_t)batch * sizeof(int32_t)));
+            w->order_frames = (size_t)batch;
         }
         {
             const long long per = v2 ? v2_scratch_doubles(*g)
@@ -922,6 +939,15 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     }
     if (v2 && !codes_ready)
         HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
+    {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order)
+        const char *e = std::getenv("QLDPC_ORDER");
+        if (!(e && std::strcmp(e, "0") == 0) && batch > 1) {
+            HIP_TRY(launch_frame_order(g->n, g->m, dg->ell_col, dg->row_deg, batch, synd, llr,
+                                       v2 ? w->codes : nullptr, w->palette, w->pal_ok, w->fweight, w->forder,
+                                       stream));
+            a.frame_order = w->forder;
+        }
+    }
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
 #ifdef QL_PHASE_STAMPS
     const size_t nst = (size_t)wgs * (block_threads(*g) / 64) * NUM_STAMPS;
@@ -1157,9 +1183,13 @@ int qldpc_decode_batch(qldpc_graph *g, const qldpc_params *p, int32_t batch, con
         const int f0 = gi * per, f1 = std::min(batch, f0 + per), nb = f1 - f0;
         if (nb <= 0) return;
         const size_t n = (size_t)g->n, m = (size_t)g->m;
+        // One call at a time per device owns the staging buffers and their
+        // stream, from the copy-in to the completed copy-out: concurrent host
+        // threads on one shared graph (the reference's thread pool over
+        // trials) serialise here instead of overwriting each other's frames.
         auto body = [&]() -> int {
             HIP_TRY(hipSetDevice(dg->device));
-            std::lock_guard<std::mutex> lk(dg->mu);  // the device's staging buffers
+            std::lock_guard<std::mutex> io_lk(dg->io_mu);
             HostIO &io = dg->io;
             if (!io.stream) HIP_TRY(hipStreamCreateWithFlags(&io.stream, hipStreamNonBlocking));
             if ((size_t)nb > io.cap_frames) {
@@ -1171,28 +1201,22 @@ int qldpc_decode_batch(qldpc_graph *g, const qldpc_params *p, int32_t batch, con
             }
             HIP_TRY(hipMemcpyAsync(io.llr, llr + f0 * n, nb * n * sizeof(double), hipMemcpyHostToDevice, io.stream));
             HIP_TRY(hipMemcpyAsync(io.synd, syndrome + f0 * m, nb * m, hipMemcpyHostToDevice, io.stream));
-            return QLDPC_OK;
-        };
-        int r = body();
-        if (!r) {
-            HostIO &io = dg->io;
-            r = decode_on(g, dg, p, nb, io.llr, io.synd, io.bits, io.iters, io.ok, posterior_out ? io.post : nullptr,
-                          io.stream);
-            if (!r) {
-                auto fin = [&]() -> int {
-                    HIP_TRY(hipMemcpyAsync(bits_out + f0 * n, io.bits, nb * n, hipMemcpyDeviceToHost, io.stream));
-                    HIP_TRY(hipMemcpyAsync(iters_out + f0, io.iters, nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                           io.stream));
-                    HIP_TRY(hipMemcpyAsync(synd_ok_out + f0, io.ok, nb, hipMemcpyDeviceToHost, io.stream));
-                    if (posterior_out)
-                        HIP_TRY(hipMemcpyAsync(posterior_out + f0 * n, io.post, nb * n * sizeof(double),
-                                               hipMemcpyDeviceToHost, io.stream));
-                    HIP_TRY(hipStreamSynchronize(io.stream));
-                    return split_check(g, dg, io.stream);
-                };
-                r = fin();
+            int r = decode_on(g, dg, p, nb, io.llr, io.synd, io.bits, io.iters, io.ok,
+                              posterior_out ? io.post : nullptr, io.stream);
+            if (r) {
+                (void)hipStreamSynchronize(io.stream);  // nothing of this call stays in flight
+                return r;
             }
-        }
+            HIP_TRY(hipMemcpyAsync(bits_out + f0 * n, io.bits, nb * n, hipMemcpyDeviceToHost, io.stream));
+            HIP_TRY(hipMemcpyAsync(iters_out + f0, io.iters, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, io.stream));
+            HIP_TRY(hipMemcpyAsync(synd_ok_out + f0, io.ok, nb, hipMemcpyDeviceToHost, io.stream));
+            if (posterior_out)
+                HIP_TRY(hipMemcpyAsync(posterior_out + f0 * n, io.post, nb * n * sizeof(double), hipMemcpyDeviceToHost,
+                                       io.stream));
+            HIP_TRY(hipStreamSynchronize(io.stream));
+            return split_check(g, dg, io.stream);
+        };
+        const int r = body();
         rcs[gi] = r;
         if (r) errs[gi] = g_last_error;
     };

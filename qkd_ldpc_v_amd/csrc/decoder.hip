@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
     uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
     for (;;) {
-        if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+        if (tid == 0) *s_frame = claim_frame(a);
         STAMP(ST_SETUP);
         __syncthreads();
         STAMP(ST_SETUP_WAIT);

@@ -75,6 +75,7 @@ struct DecodeArgs {
     double *post;           // [batch][n] or nullptr
     // scheduling / scratch
     int *frame_counter;
+    const int32_t *frame_order;   // [batch] claim order (order.hip); nullptr: index order
     double *scratch;              // per-workgroup scratch (variants 1, 2)
     long long scratch_wg_doubles; // doubles per workgroup
     uint64_t *stamps;             // diagnostic build only: [wg][wave][NUM_STAMPS]
@@ -131,6 +132,13 @@ struct DecodeArgs {
     long long rows_wg_offset;
 };
 
+// The persistent decoders' frame claim: the next frame of the launch's claim
+// order (order.hip; results never depend on it).  >= batch: none left.
+__device__ __forceinline__ int claim_frame(const DecodeArgs &a) {
+    const int c = atomicAdd(a.frame_counter, 1);
+    return (a.frame_order && c < a.batch) ? a.frame_order[c] : c;
+}
+
 // Dynamic LDS bytes / scratch doubles a variant needs for this shape.
 size_t lds_bytes_for(int variant, int n, int m, int T);
 long long scratch_doubles_for(int variant, int n, int m, int T, int EPL);
@@ -168,6 +176,13 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
                                   const uint8_t *palice, const uint8_t *pbob, const double *log_p, uint8_t *alice_ext,
                                   double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
                                   hipStream_t stream);
+// Claim order of a batch: frames by ascending weight of the channel decision's
+// syndrome mismatch (order.hip).  llr is read only for frames without codes.
+size_t frame_weight_lds(int n);
+hipError_t launch_frame_order(int n, int m, const int32_t *ell_col, const int32_t *row_deg, int batch,
+                              const uint8_t *synd, const double *llr, const uint8_t *codes,
+                              const double *palette, const uint8_t *pal_ok, int32_t *weight, int32_t *order,
+                              hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
                              uint8_t *match, hipStream_t stream);

@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if (slot < a.split_slots) {
                     int *pub = a.split_pub + si;
                     if (rank == 0) {
-                        f = atomicAdd(a.frame_counter, 1);
+                        f = claim_frame(a);
                         __hip_atomic_store(pub, f + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
                         int v, spins = 0;
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 s_part[1] = si;
             }
         } else {
-            if (tid == 0) *s_frame = atomicAdd(a.frame_counter, 1);
+            if (tid == 0) *s_frame = claim_frame(a);
         }
         STAMP(ST_SETUP);
         __syncthreads();

@@ -30,7 +30,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import ALGORITHM_NAMES, Params, check, lib
+from ._lib import ALGORITHM_NAMES, Params, check, lib, log_p
 from .graph import Graph, adapt_code_rate, load_matrix, trial_seeds, xoshiro_state
 
 EPSILON = 1e-6  # src/config.hpp:199
@@ -203,6 +203,25 @@ class Config:
                                "efficiency": (float(f["begin"]), float(f["end"]), float(f["step"]))})
                 if not rr:
                     raise ConfigError("Array with code rate(R) and adaptation parameters ranges is empty!")
+                for e in rr:  # src/config.cpp:327-354, same order and messages
+                    if not 0 < e["code_rate"] < 1:
+                        raise ConfigError("Code rate(R) must be: 0 < R < 1!")
+                    db, de, ds = e["delta"]
+                    if not (0 < db < 1 and 0 < de < 1) or db > de:
+                        raise ConfigError("Invalid delta begin or end parameters. Delta must be: 0 < delta < 1, "
+                                          "and begin cannot be larger than end!")
+                    if not ds > 0:
+                        raise ConfigError("Delta step must be > 0!")
+                    if db != de and ds - EPSILON > de - db:
+                        raise ConfigError("Delta step is too large.")
+                    fb, fe, fs = e["efficiency"]
+                    if fb < 1 or fe < 1 or fb > fe:
+                        raise ConfigError("Invalid efficiency begin or end parameters. Efficiency(f_EC) must be: "
+                                          "f_EC >= 1, and begin cannot be larger than end!")
+                    if not fs > 0:
+                        raise ConfigError("Efficiency step must be > 0!")
+                    if fb != fe and fs - EPSILON > fe - fb:
+                        raise ConfigError("Efficiency step is too large.")
                 cfg.adaptation_ranges = _sorted_by_rate(rr)
             else:
                 mm = []
@@ -393,7 +412,7 @@ def run(cfg: Config, mats, combos, device: int = 0, max_batch: int = 4096, log=p
                                                  seed_add=sim)
             else:
                 q_acc = trials_device(H.n, c.config_qber, ds, ta, tb, seed_add=sim)
-            lp = torch.full((nb,), float(np.log((1.0 - q_acc) / q_acc)), dtype=torch.float64, device=dev)
+            lp = torch.full((nb,), log_p(q_acc), dtype=torch.float64, device=dev)  # the C library's log (:1043)
             llr = torch.empty((nb, H.n), dtype=torch.float64, device=dev)
             syn = torch.empty((nb, H.m), dtype=torch.uint8, device=dev)
             bits = torch.empty_like(ta)

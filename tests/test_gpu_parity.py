@@ -484,3 +484,45 @@ def test_zero_batch_and_single_frame(gpu_available):
     out = g.decode(Q.Params(Q.SPA, 50, True, 100.0), llr[:0], s[:0])
     assert out.bits.shape == (0, H.n)
     assert_parity("c1_n1024_m220.alist", Q.SPA, 0, 0, qber=0, batch=1, llr=llr, synd=s)
+
+
+@pytest.mark.parametrize("name,alg,prim,sec", [("c1_n1024_m220.alist", Q.SPA, 0.0, 0.0),
+                                               ("c3_n10240_m1801.alist", Q.OMSA, 0.77, 0.0)])
+def test_host_threads_share_one_graph(gpu_available, name, alg, prim, sec):
+    """qldpc_decode_batch called concurrently by host threads on ONE graph (the
+    reference's thread pool over trials, src/simulation.cpp:740-746): calls of
+    different sizes (the staging buffers grow under other threads), with and
+    without posteriors; every frame must equal the oracle's."""
+    import threading
+
+    H = load_fixture(name)
+    total = 8 * 6 * 5
+    _, _, llr, synd = frames(H, 0.02 if alg == Q.SPA else 0.015, total, seed=99)
+    O = Oracle(H)
+    prm = (alg, 50, True, 100.0, prim, sec)
+    ob, oi, ok, op = O.decode_batch(O.params(*prm), llr, synd, threads=16, posterior=True)
+    g = Q.Graph(H)
+    errors = []
+
+    def worker(t):
+        try:
+            f = t * 30
+            for call, size in enumerate((1, 7, 2, 12, 3, 5)):
+                sl = slice(f, f + size)
+                out = g.decode(Q.Params(*prm), llr[sl], synd[sl], posterior=(call % 2 == 0))
+                for j, fr in enumerate(range(sl.start, sl.stop)):
+                    same = (np.array_equal(out.bits[j], ob[fr]) and out.iterations[j] == oi[fr]
+                            and out.synd_ok[j] == ok[fr]
+                            and (out.posterior is None or bits_equal_nan(out.posterior[j], op[fr])))
+                    if not same:
+                        errors.append((t, call, fr))
+                f += size
+        except Exception as e:  # surfaced below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, f"{len(errors)} frames/calls differ; first {errors[:3]}"

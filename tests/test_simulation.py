@@ -59,6 +59,52 @@ def test_config_errors_mirror_the_reference(tmp_path):
         S.Config.load(str(p))
 
 
+@pytest.mark.parametrize("field,value,msg", [
+    ("code_rate", 1.0, "Code rate\\(R\\) must be: 0 < R < 1!"),
+    ("delta", {"begin": 0.2, "end": 0.1, "step": 0.01}, "Invalid delta begin or end parameters"),
+    ("delta", {"begin": 0.0, "end": 0.1, "step": 0.01}, "Invalid delta begin or end parameters"),
+    ("delta", {"begin": 0.05, "end": 0.1, "step": 0.0}, "Delta step must be > 0!"),
+    ("delta", {"begin": 0.05, "end": 0.1, "step": 0.2}, "Delta step is too large."),
+    ("efficiency", {"begin": 0.9, "end": 1.2, "step": 0.1}, "Invalid efficiency begin or end parameters"),
+    ("efficiency", {"begin": 1.3, "end": 1.2, "step": 0.1}, "Invalid efficiency begin or end parameters"),
+    ("efficiency", {"begin": 1.0, "end": 1.2, "step": 0.0}, "Efficiency step must be > 0!"),
+    ("efficiency", {"begin": 1.0, "end": 1.2, "step": 0.5}, "Efficiency step is too large."),
+])
+def test_adaptation_ranges_validation_mirrors_the_reference(tmp_path, field, value, msg):
+    """code_rate_adaptation_parameters_ranges checks of src/config.cpp:327-354."""
+    c = json.load(open(cfg_path("adaptive_t")))
+    ra = c["code_rate_adaptation_parameters"]
+    ra["use_adaptation_parameters_ranges"] = True
+    good = {"code_rate": 0.8, "delta": {"begin": 0.05, "end": 0.1, "step": 0.01},
+            "efficiency": {"begin": 1.0, "end": 1.2, "step": 0.1}}
+    ra["code_rate_adaptation_parameters_ranges"] = [good]
+    p = tmp_path / "ok.json"
+    p.write_text(json.dumps(c))
+    assert S.Config.load(str(p)).adaptation_ranges[0]["delta"] == (0.05, 0.1, 0.01)
+    bad = dict(good)
+    bad[field] = value
+    ra["code_rate_adaptation_parameters_ranges"] = [good, bad]
+    p.write_text(json.dumps(c))
+    with pytest.raises(S.ConfigError, match=msg):
+        S.Config.load(str(p))
+
+
+def test_driver_log_p_is_the_c_library_log():
+    """The driver's a-priori LLR magnitude is log((1-q)/q) by the C library, as
+    the reference computes it (src/qkd_ldpc_algorithm.cpp:1043): at n=10240,
+    n_err=229 numpy's log differs from it by one ulp on some hosts, which would
+    change every LLR of the frame."""
+    for n, ne in ((10240, 229), (10240, 689), (102400, 2290), (102400, 5764), (1024, 13)):
+        q = ne / n
+        want = Q.log_p(q)
+        assert S.log_p(q) == want
+        import ctypes
+        libm = ctypes.CDLL("libm.so.6")
+        libm.log.restype = ctypes.c_double
+        libm.log.argtypes = [ctypes.c_double]
+        assert want == libm.log((1.0 - q) / q)
+
+
 def test_rate_adapted_combinations_match_oracle_chain(tmp_path):
     cfg = S.Config.load(cfg_path("adaptive_t"))
     d = mtrx_dir(tmp_path, "c5_n10240_m2048.sp2", "c5_n10240_m2048.untp")
@@ -120,7 +166,7 @@ def _oracle_stats(H, alg, prim, sec, thr, max_it, q, seeds, sim, punct=None, sho
         sd = (int(sd) + sim) & 0xFFFFFFFFFFFFFFFF
         if punct is None:
             a, b, qa = P.trial(H.n, q, sd)
-            lp = np.log((1 - qa) / qa)
+            lp = Q.log_p(qa)  # the C library log, as the driver and the reference (:1043)
             llrs.append(np.where(b != 0, -lp, lp))
             alices.append(a)
         else:
