@@ -4,7 +4,13 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := qkd_ldpc_v_amd
 CSRC := $(PKG)/csrc
-HIPFLAGS := --offload-arch=$(ARCH) $(EXTRA_HIPFLAGS) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result
+# -amdgpu-atomic-optimizer-strategy=None: the atomic optimizer rewrites a uniform
+# atomic into a single-lane block (mbcnt + narrowed exec); with this register
+# pressure LLVM (ROCm 7.2) placed a VGPR spill store inside such a block in the
+# split-frame kernel, so 63 lanes reloaded an unwritten slot.
+# Every atomic here is already issued by one lane on purpose.
+HIPFLAGS := --offload-arch=$(ARCH) $(EXTRA_HIPFLAGS) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result \
+            -mllvm -amdgpu-atomic-optimizer-strategy=None
 LIB := $(PKG)/libqkdldpc_hip.so
 ORACLE := oracle/libqkdldpc_oracle.so
 HOSTCHK := $(PKG)/host/host_mirror_check

@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
         STAMP(ST_SETUP);
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
-        const int f = *s_frame;
+        const int f = __builtin_amdgcn_readfirstlane(*s_frame);  // wave-uniform: SGPR addressing
         if (f >= a.batch) break;
         const double *llr = a.llr + (size_t)f * n;
         const uint8_t *sy = a.synd + (size_t)f * m;

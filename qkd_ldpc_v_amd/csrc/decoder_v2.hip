@@ -235,7 +235,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         STAMP(ST_SETUP);
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
-        const int f = *s_frame;
+        // wave-uniform by construction: readfirstlane lets the compiler keep
+        // every per-frame address (llr / stage buffer descriptors) in SGPRs
+        // instead of VGPRs with waterfall loops around each access
+        const int f = __builtin_amdgcn_readfirstlane(*s_frame);
         if (f >= a.batch) break;
         // SPLIT: this part's lanes, waves, metadata and rows; the group barrier
         const int rank = SPLIT ? __builtin_amdgcn_readfirstlane(s_part[0]) : 0;
