@@ -349,11 +349,16 @@ __global__ void __launch_bounds__(256) keys_match_kernel(int n, const uint8_t *a
 }
 
 __global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, const double *in, double *out) {
+    __shared__ ql_exact::Expm1Class ctab[ql_exact::EXPM1_CLASSES];  // fn 8: the SPA scan's table form
+    if (threadIdx.x < ql_exact::EXPM1_CLASSES) ctab[threadIdx.x] = ql_exact::expm1_class(threadIdx.x + ql_exact::EXPM1_K_MIN);
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const double x = in[i];
     double y;
+    int flag = 0;
     switch (fn) {
+    case 8: y = ql_exact::tanh_half_clip_t(x, 44.0, 1.0, &flag, ctab); break;  // tanh(clip(x, inf) / 2.), tanh(22) = 1
     case 0: y = ql_exact::tanh_exact(x); break;
     case 1: y = ql_exact::atanh_exact(x); break;
     case 2: y = ql_exact::expm1_exact(x); break;

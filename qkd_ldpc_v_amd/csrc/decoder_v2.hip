@@ -47,7 +47,7 @@ constexpr int V2_A0_ENTRIES = 64;
 // memory and the palette indices are read from the 2-bit global codes; LDS
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
-    size_t total, rows, rowflag, tail, tailneg, a0tab, msl, codes, palette, bytes;
+    size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, bytes;
     __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
@@ -58,6 +58,7 @@ struct V2Layout {
         tail = o;     // (min-sum: a lane's tail aggregate is parked in its row's rowAB entry)
         tailneg = o;
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
+        ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * 16));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         bytes = o;
     }
@@ -194,6 +195,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const int up = (lane == 0) ? 0 : lane - 1;
     int epoch = 0;
     if (tid == 0) *s_flag = 0;
+    // SPA: the expm1 class table of tanh_half_clip_t, once per workgroup (the
+    // frame loop's first barrier orders it before any scan)
+    const ql_exact::Expm1Class *const ctab = reinterpret_cast<const ql_exact::Expm1Class *>(smem + L.ctab);
+    if constexpr (ALG == 0) {
+        if (tid < ql_exact::EXPM1_CLASSES)
+            reinterpret_cast<ql_exact::Expm1Class *>(smem + L.ctab)[tid] = ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN);
+    }
 #ifdef QL_PHASE_STAMPS
     uint64_t st_acc[NUM_STAMPS];
     for (int i = 0; i < NUM_STAMPS; ++i) st_acc[i] = 0;
@@ -677,7 +685,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     // into tanh_half_clip with the iteration's (lim, thr).
                     const double b = tv - c2b.get(k);
                     double t = b;
-                    if (compute) t = ql_exact::tanh_half_clip(b, lim_it, tlim_it, &div_unsafe);  // tanh(b2c / 2.) (:60)
+                    if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // tanh(b2c / 2.) (:60)
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;

@@ -663,6 +663,82 @@ QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
     return C + div_rn_safe(num, y + 2.0);
 }
 
+// Table form of the per-class constants above.  They depend on k alone, and
+// the common path only reaches k in [-3, 63] (u in (-2, 0] or [2, 44)), so a
+// 67-entry table indexed by k + 3 holds X3, X4 and B (high words; the low
+// words are 0) and the exponent addend k << 20: one 16-byte LDS read replaces
+// the class arithmetic and its selects.  Same constants, same IEEE operations.
+struct alignas(16) Expm1Class {
+    uint32_t x3_hi, x4_hi, b_hi, k20;
+};
+constexpr int EXPM1_K_MIN = -3, EXPM1_K_MAX = 63, EXPM1_CLASSES = EXPM1_K_MAX - EXPM1_K_MIN + 1;
+QL_HD Expm1Class expm1_class(int32_t k) {
+    const uint32_t ku = (uint32_t)k;
+    const bool fcls = (ku - 20u) <= 36u;
+    const bool far = (ku + 1u) > 57u;
+    uint32_t a_hi = 0x3ff00000u - (0x200000u >> (ku & 31u));
+    a_hi = (k == 0) ? 0x80000000u : a_hi;
+    a_hi = (k == -1) ? 0xbff00000u : a_hi;
+    Expm1Class c;
+    c.x3_hi = fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u;
+    c.x4_hi = fcls ? 0x3ff00000u : a_hi;
+    c.b_hi = far ? 0xbff00000u : 0x80000000u;
+    c.k20 = ku << 20;
+    return c;
+}
+
+// tanh_half_common with the class constants from `tab` (EXPM1_CLASSES
+// entries, tab[i] = expm1_class(i + EXPM1_K_MIN)).  Lanes outside the common
+// path (the callers' rare branch recomputes them) read a clamped entry.
+QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *tab) {
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double Q1 = -3.33333333333331316428e-02, Q2 = 1.58730158725481460165e-03;
+    const double Q3 = -7.93650757867487942473e-05, Q4 = 4.00821782732936239552e-06;
+    const double Q5 = -2.01099218183624371326e-07;
+
+    const uint32_t jb = hi_word(b);
+    const uint32_t ib = jb & 0x7fffffffu;
+    const uint32_t sx = jb & 0x80000000u;
+    const bool big = ib >= 0x40000000u;
+    const double ab = __builtin_fabs(b);
+    const double u = big ? ab : -ab;
+    double kf = invln2 * u + (big ? 0.5 : -0.5);
+#if !defined(__HIP_DEVICE_COMPILE__)
+    kf = (kf > 1e6 || kf < -1e6 || kf != kf) ? 0.0 : kf;
+#endif
+    int32_t k = (ib < 0x3FF0A2B2u) ? -1 : (int32_t)kf;
+    k = (ib > 0x3fd62e42u) ? k : 0;
+    const int32_t kc = k < EXPM1_K_MIN ? EXPM1_K_MIN : (k > EXPM1_K_MAX ? EXPM1_K_MAX : k);
+    const Expm1Class cl = tab[kc - EXPM1_K_MIN];  // issued early, used after the division
+    const double t = (double)k;
+    const double hi = u - t * ln2_hi;
+    const double lo = t * ln2_lo;
+    const double xr = hi - lo;
+    const double c = (hi - xr) - lo;
+    const double hfx = 0.5 * xr;
+    const double hxs = xr * hfx;
+    const double R1 = 1.0 + hxs * Q1;
+    const double h2 = hxs * hxs;
+    const double R2 = Q2 + hxs * Q3;
+    const double h4 = h2 * h2;
+    const double R3 = Q4 + hxs * Q5;
+    const double r1 = R1 + h2 * R2 + h4 * R3;
+    const double t3 = 3.0 - r1 * hfx;
+    const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
+    const double e2 = (xr * (e - c) - c) - hxs;
+    const double X3 = from_words(cl.x3_hi, 0u);
+    const double X4 = from_words(cl.x4_hi, 0u);
+    const double B = from_words(cl.b_hi, 0u);
+    const double ypre = (xr - (e2 + X3)) + X4;
+    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + B;
+    const double num = big ? from_words(0xc0000000u ^ sx, 0u) : from_words(hi_word(y) ^ 0x80000000u ^ sx, lo_word(y));
+    const double C = from_words(big ? (0x3ff00000u ^ sx) : 0x80000000u, 0u);
+    *ib_out = ib;
+    return C + div_rn_safe(num, y + 2.0);
+}
+
 QL_HD double tanh_half_dec(double b) {
     uint32_t ib;
     double z = tanh_half_common(b, &ib);
@@ -687,6 +763,20 @@ QL_HD double tanh_half_clip(double b, double lim, double t_lim, int *tiny_or_nan
     uint32_t ib;
     double z = tanh_half_common(b, &ib);
     const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);  // tiny, |b| >= lim, NaN
+    QL_RARE(special) {
+        const double x = b / 2.;
+        z = (ib < 0x3c900000u) ? x * (1.0 + x) : __builtin_copysign(t_lim, b);
+        z = (b != b) ? x + x : z;
+        if (ib < 0x3c900000u || b != b) *tiny_or_nan = 1;
+    }
+    return z;
+}
+
+// tanh_half_clip on tanh_half_common_t (the table form).
+QL_HD double tanh_half_clip_t(double b, double lim, double t_lim, int *tiny_or_nan, const Expm1Class *tab) {
+    uint32_t ib;
+    double z = tanh_half_common_t(b, &ib, tab);
+    const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);
     QL_RARE(special) {
         const double x = b / 2.;
         z = (ib < 0x3c900000u) ? x * (1.0 + x) : __builtin_copysign(t_lim, b);

@@ -82,12 +82,14 @@ def test_device_exact_math_bitwise(gpu_available):
     refs = {0: math.tanh, 2: math.expm1}
     d_in = torch.from_numpy(xs).cuda()
     d_out = torch.empty_like(d_in)
-    for fn, name in ((0, "tanh"), (1, "atanh"), (2, "expm1"), (3, "log1p"), (6, "tanh_dec"), (7, "atanh_dec")):
+    for fn, name in ((0, "tanh"), (1, "atanh"), (2, "expm1"), (3, "log1p"), (6, "tanh_dec"), (7, "atanh_dec"),
+                     (8, "tanh_half_clip_t")):
         Q._lib.check(Q.lib().qldpc_selftest_math_device(fn, xs.size, d_in.data_ptr(), d_out.data_ptr(), None),
                      "selftest")
         torch.cuda.synchronize()
         got = d_out.cpu().numpy()
-        f = {0: math.tanh, 1: math.atanh, 2: math.expm1, 3: math.log1p, 6: math.tanh, 7: math.atanh}[fn]
+        f = {0: math.tanh, 1: math.atanh, 2: math.expm1, 3: math.log1p, 6: math.tanh, 7: math.atanh,
+             8: lambda v: math.tanh(v / 2.)}[fn]  # 8: the SPA scan's table form of tanh(b2c / 2.)
 
         def ref(x):
             try:

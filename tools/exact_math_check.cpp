@@ -21,6 +21,9 @@ static inline uint64_t sm64(uint64_t &s) {
 }
 static inline double u01(uint64_t &s) { return (sm64(s) >> 11) * 0x1.0p-53; }
 static thread_local int dummy_flag = 0;
+// the decoder's expm1 class table (exact_math.h: tanh_half_common_t)
+static ql_exact::Expm1Class g_ctab[ql_exact::EXPM1_CLASSES];
+static double tanh_t(double b, double lim, double tl) { return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, g_ctab); }
 static inline bool same(double a, double b) {
     if (a != a && b != b) return true;
     uint64_t x, y; memcpy(&x, &a, 8); memcpy(&y, &b, 8); return x == y;
@@ -40,8 +43,9 @@ int main(int argc, char **argv) {
     long per = argc > 1 ? atol(argv[1]) : 1000000;
     uint64_t seed0 = argc > 2 ? strtoull(argv[2], 0, 10) : 12345;
     unsigned nt = std::thread::hardware_concurrency(); if (!nt) nt = 4;
-    const char *names[14] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec", "tanh_half_dec", "atanh2_dec", "tanh_half_clip", "atanh2_clip"};
-    std::atomic<long> bad[14]; for (auto &b : bad) b = 0;
+    for (int i = 0; i < ql_exact::EXPM1_CLASSES; ++i) g_ctab[i] = ql_exact::expm1_class(i + ql_exact::EXPM1_K_MIN);
+    const char *names[15] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec", "tanh_half_dec", "atanh2_dec", "tanh_half_clip", "atanh2_clip", "tanh_half_clip_t"};
+    std::atomic<long> bad[15]; for (auto &b : bad) b = 0;
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] {
         uint64_t s = seed0 * 1000003 + t;
@@ -70,6 +74,7 @@ int main(int argc, char **argv) {
                 const double lim = T < 44.0 ? T : 44.0;
                 const double rt = std::tanh(ql_exact::clip_thr(b, T) / 2.);
                 if (!same(ql_exact::tanh_half_clip(b, lim, std::tanh(lim / 2.), &dummy_flag), rt)) { if (bad[12]++ < 5) printf("tanh_half_clip b=%a T=%g got=%a ref=%a\n", b, T, ql_exact::tanh_half_clip(b, lim, std::tanh(lim / 2.), &dummy_flag), rt); }
+                if (!same(tanh_t(b, lim, std::tanh(lim / 2.)), rt)) { if (bad[14]++ < 5) printf("tanh_half_clip_t b=%a T=%g got=%a ref=%a\n", b, T, tanh_t(b, lim, std::tanh(lim / 2.)), rt); }
                 const double Ta = (i % 3 == 0) ? 100.0 : (i % 3 == 1) ? 3.0 : HUGE_VAL;
                 const double ra = ql_exact::clip_thr(2. * std::atanh(y), Ta);
                 if (!same(ql_exact::atanh2_clip(y, Ta, 2. * std::atanh(0x1.fffffffffffffp-1)), ra)) { if (bad[13]++ < 5) printf("atanh2_clip p=%a T=%g got=%a ref=%a\n", y, Ta, ql_exact::atanh2_clip(y, Ta, 2. * std::atanh(0x1.fffffffffffffp-1)), ra); }
@@ -78,7 +83,7 @@ int main(int argc, char **argv) {
     });
     for (auto &x : th) x.join();
     long tot = 0;
-    for (int f = 0; f < 14; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
+    for (int f = 0; f < 15; ++f) { printf("%s mismatches: %ld / %ld\n", names[f], bad[f].load(), per * (long)nt); tot += bad[f]; }
     // Sweep the high words around every branch boundary of the four functions.
     const uint32_t bounds[] = {0x3FDA827A, 0xbfd2bec3, 0xbfd2bec4, 0x3e200000, 0x3c900000, 0x43400000, 0x3ff00000,
                                0x3fd62e42, 0x3FF0A2B2, 0x4043687A, 0x40862E42, 0x40360000, 0x3c800000, 0x3fe00000,
@@ -93,17 +98,19 @@ int main(int argc, char **argv) {
                     const uint32_t hi = (base + d) ^ (sg ? 0x80000000u : 0u);
                     const uint64_t b = ((uint64_t)hi << 32) | lo;
                     double x; memcpy(&x, &b, 8);
-                    const double r[14] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
+                    const double r[15] = {std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
                                          std::tanh(x), std::atanh(x), std::expm1(x), std::log1p(x),
                                          std::tanh(x), std::atanh(x), std::tanh(x / 2.), 2. * std::atanh(x),
                                          std::tanh(ql_exact::clip_thr(x, 100.0) / 2.),
-                                         ql_exact::clip_thr(2. * std::atanh(x), 100.0)};
-                    const double g[14] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
+                                         ql_exact::clip_thr(2. * std::atanh(x), 100.0),
+                                         std::tanh(ql_exact::clip_thr(x, 100.0) / 2.)};
+                    const double g[15] = {ql_exact::tanh_exact(x), ql_exact::atanh_exact(x), ql_exact::expm1_exact(x),
                                          ql_exact::log1p_exact(x), ql_exact::tanh_bf(x), ql_exact::atanh_bf(x),
                                          ql_exact::expm1_bf(x), ql_exact::log1p_bf(x), ql_exact::tanh_dec(x),
                                          ql_exact::atanh_dec(x), ql_exact::tanh_half_dec(x), ql_exact::atanh2_dec(x),
-                                         ql_exact::tanh_half_clip(x, 44.0, std::tanh(22.0), &dummy_flag), ql_exact::atanh2_clip(x, 100.0, 2. * std::atanh(0x1.fffffffffffffp-1))};
-                    for (int f = 0; f < 14; ++f) {
+                                         ql_exact::tanh_half_clip(x, 44.0, std::tanh(22.0), &dummy_flag), ql_exact::atanh2_clip(x, 100.0, 2. * std::atanh(0x1.fffffffffffffp-1)),
+                                         tanh_t(x, 44.0, std::tanh(22.0))};
+                    for (int f = 0; f < 15; ++f) {
                         ++nb;
                         if (!same(r[f], g[f]) && bb++ < 5) printf("boundary %s x=%a ref=%a got=%a\n", names[f], x, r[f], g[f]);
                     }
@@ -123,6 +130,9 @@ int main(int argc, char **argv) {
                     const double lim = T < 44.0 ? T : 44.0;
                     const double rt = std::tanh(ql_exact::clip_thr(v, T) / 2.);
                     const double gt = ql_exact::tanh_half_clip(v, lim, std::tanh(lim / 2.), &dummy_flag);
+                    const double gt2 = tanh_t(v, lim, std::tanh(lim / 2.));
+                    nb += 1;
+                    if (!same(rt, gt2) && bb++ < 20) printf("edge tanh_half_clip_t v=%a T=%g ref=%a got=%a\n", v, T, rt, gt2);
                     const double ra = ql_exact::clip_thr(2. * std::atanh(v), T);
                     const double ga = ql_exact::atanh2_clip(v, T, C_TOP);
                     nb += 2;
