@@ -733,10 +733,14 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     const double B = from_words(cl.b_hi, 0u);
     const double ypre = (xr - (e2 + X3)) + X4;
     const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + B;
-    const double num = big ? from_words(0xc0000000u ^ sx, 0u) : from_words(hi_word(y) ^ 0x80000000u ^ sx, lo_word(y));
-    const double C = from_words(big ? (0x3ff00000u ^ sx) : 0x80000000u, 0u);
+    // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
+    // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
+    // end (round-to-nearest is symmetric; the sum is never 0 on this path).
+    const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
+    const double C = from_words(big ? 0x3ff00000u : 0x80000000u, 0u);
+    const double zp = C + div_rn_safe(num, y + 2.0);
     *ib_out = ib;
-    return C + div_rn_safe(num, y + 2.0);
+    return from_words(hi_word(zp) ^ sx, lo_word(zp));
 }
 
 QL_HD double tanh_half_dec(double b) {
@@ -813,15 +817,13 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     int32_t k = (hu >> 20) - 1023;                 // >= 0
     const double cn = (k > 0) ? 1.0 - (u0 - a) : a - (u0 - 1.0);
     double c = div_rn_safe(cn, u0);
-    hu &= 0x000fffff;
-    const bool up = hu >= 0x6a09e;
-    const double u = with_hi_word(u0, (uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)));
+    const uint32_t hm = (uint32_t)hu & 0x000fffffu;
+    const bool up = hm >= 0x6a09eu;
+    const double u = with_hi_word(u0, hm | (up ? 0x3fe00000u : 0x3ff00000u));
     k = up ? k + 1 : k;
-    hu = up ? (0x00100000 - hu) >> 2 : hu;
     double f = u - 1.0;
     f = k0 ? a : f;
     k = k0 ? 0 : k;
-    hu = k0 ? 1 : hu;
     c = k0 ? 0.0 : c;
     const double hfsq = 0.5 * f * f;
     const double dk = (double)k;
@@ -837,11 +839,18 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
     // k == 0 through the k != 0 formula (dk = c = 0): see atanh_dec
     double y = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
-    QL_RARE(hu == 0) {                             // |f| < 2^-20
-        const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
-        const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
-        const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
-        y = (f == 0.0) ? yzero : ysmall;
+    // s_log1p.c's |f| < 2^-20 case is hu == 0 with hu = k0 ? 1 : (up ? (0x100000 -
+    // hm) >> 2 : hm), i.e. !k0 && (hm == 0 || hm >= 0xffffd): one test on hm
+    // admits exactly those four values (k0 lanes included), the exact
+    // condition is applied inside.
+    QL_RARE(((hm + 3u) & 0xfffffu) < 4u) {
+        const uint32_t hu2 = k0 ? 1u : (up ? (0x00100000u - hm) >> 2 : hm);
+        if (hu2 == 0) {                            // |f| < 2^-20
+            const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+            const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
+            const double yzero = (k == 0) ? 0.0 : dk * ln2_hi + (c + dk * ln2_lo);
+            y = (f == 0.0) ? yzero : ysmall;
+        }
     }
     *ia_out = ia;
     return __builtin_copysign(y, p);               // 2 * copysign(0.5 * y, p)

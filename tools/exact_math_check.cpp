@@ -140,6 +140,32 @@ int main(int argc, char **argv) {
                     if (!same(ra, ga) && bb++ < 20) printf("edge atanh2_clip v=%a T=%g ref=%a got=%a\n", v, T, ra, ga);
                 }
     }
+    // atanh's log1p argument a = 2|p| / (1 - |p|) (or the small form) next to
+    // every power of two: u0 = 1 + a with its high mantissa word near 0 or
+    // 0xfffff (s_log1p.c's |f| < 2^-20 case and the up/down normalisation)
+    {
+        const double C_TOP = 2. * std::atanh(0x1.fffffffffffffp-1);
+        long pb = 0;
+        for (int j = -30; j <= 54; ++j)
+            for (int side = -1; side <= 1; side += 2)
+                for (int d = 0; d < 400; ++d) {
+                    const double u0 = std::ldexp(1.0, j > 0 ? j : 0) * (side < 0 ? (1.0 - std::ldexp((double)d, -53)) : (1.0 + std::ldexp((double)d, -52)));
+                    const double a = (j > 0) ? u0 - 1.0 : std::ldexp(1.0 + std::ldexp((double)d * side, -52), j);
+                    for (int e = -2; e <= 2; ++e) {
+                        double pv = a / (a + 2.0);
+                        for (int t = 0; t < (e < 0 ? -e : e); ++t) pv = std::nextafter(pv, e < 0 ? 0.0 : 2.0);
+                        for (double v : {pv, -pv}) {
+                            nb += 2;
+                            if (!same(ql_exact::atanh2_clip(v, HUGE_VAL, C_TOP), 2. * std::atanh(v)) && pb++ < 5)
+                                printf("pow2 atanh2_clip p=%a ref=%a got=%a\n", v, 2. * std::atanh(v), ql_exact::atanh2_clip(v, HUGE_VAL, C_TOP));
+                            if (!same(ql_exact::atanh2_dec(v), 2. * std::atanh(v)) && pb++ < 5)
+                                printf("pow2 atanh2_dec p=%a ref=%a got=%a\n", v, 2. * std::atanh(v), ql_exact::atanh2_dec(v));
+                        }
+                    }
+                }
+        printf("power-of-two atanh mismatches: %ld\n", pb);
+        bb += pb;
+    }
     printf("boundary mismatches: %ld / %ld\n", bb, nb);
     return (tot || bb) ? 1 : 0;
 }
