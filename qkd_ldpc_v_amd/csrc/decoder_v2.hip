@@ -445,12 +445,31 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // phase write one column), then added and written back by the
                 // lanes whose edge there is a kk-th one.
                 meta.each_group_masked(mlo, mhi, [&](int g, auto q, uint32_t) {
+                    // the group's four lane masks in one scalar load, before any
+                    // LDS access (a scalar-load wait also waits for LDS reads)
+                    uint64_t em[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) em[i] = ex[4 * g + i];
                     double tv[4];
+#ifdef QL_VN_UNMASKED_READS
 #pragma unroll
                     for (int i = 0; i < 4; ++i) tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
+#else
+                    // only the lanes whose edge there is a kk-th one read (a
+                    // quarter of them on a dv = 4 code): LDS bytes and bank
+                    // conflicts of the phase drop with the lanes
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        // (inactive lanes' tv is never used: the add below runs
+                        // under the same mask)
+                        asm("" : "=v"(tv[i]));
+                        if (__builtin_amdgcn_inverse_ballot_w64(em[i]))
+                            tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
+                    }
+#endif
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        if (__builtin_amdgcn_inverse_ballot_w64(ex[4 * g + i]))  // kpos == kk
+                        if (__builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
                             total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
                 });
                 STAMP(ST_VNK);

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summaries of a tools/profile_round.sh run for profiles/.
 
-usage: tools/round_summary.py <round_prof_dir> <tag>
-Writes profiles/r01/<tag>_{c2,c3}_pmc.json (per-launch means of every PMC
+usage: tools/round_summary.py <round_prof_dir> <tag> [round_dir, default r02]
+Writes profiles/<round_dir>/<tag>_{c2,c3}_pmc.json (per-launch means of every PMC
 pass), copies the kernel-trace stats CSVs, and refreshes profiles/pmc_<wl>.json
 (the HBM traffic bench.py reports: FETCH_SIZE doubled for gfx950 + WRITE_SIZE,
 per MI355X_MICROARCH.md's HBM section)."""
@@ -17,8 +17,9 @@ from pmc_summary import summarize  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(prof, tag):
-    out_dir = os.path.join(ROOT, "profiles", "r01")
+def main(prof, tag, rnd="r02"):
+    out_dir = os.path.join(ROOT, "profiles", rnd)
+    os.makedirs(out_dir, exist_ok=True)
     for src, dst in (("default_trace", "default_bench"), ("c2_trace", "c2_serial"), ("c3_trace", "c3_serial")):
         f = os.path.join(prof, src, "run_kernel_stats.csv")
         if os.path.exists(f):
@@ -39,7 +40,7 @@ def main(prof, tag):
             "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_* passes (separate runs, --kernel-trace only) "
                       f"of `python bench.py --workload {wl} --steps 5 --warmup 1 --no-cpu-baseline --streams 1 "
                       "--roofline-launches 0` (tools/profile_round.sh); mean over decode launches; "
-                      f"profiles/r01/{tag}_{wl}_pmc.json",
+                      f"profiles/{rnd}/{tag}_{wl}_pmc.json",
             "correction": "FETCH_SIZE (KB) doubled for gfx950 (MI355X_MICROARCH.md HBM section); WRITE_SIZE (KB) as reported",
             "FETCH_SIZE_KB": fetch,
             "WRITE_SIZE_KB": write,
@@ -52,4 +53,4 @@ def main(prof, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
