@@ -287,6 +287,23 @@ struct MetaSrcW : MetaSrc<R> {
             }
         }
     }
+    // Same, with the next group's metadata requested before this group's work
+    // (a VN phase does little per group: one memory latency per group would
+    // otherwise be exposed on every wave at once).
+    template <typename F>
+    __device__ __forceinline__ void each_group_masked_pf(uint32_t mlo, uint32_t mhi, F &&f) const {
+        auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            const uint32_t w = (4 * g < 32) ? mlo : mhi;
+            const uint32_t bits = (w >> ((4 * g) & 31)) & 15u;
+            const auto qn = (g + 1 < R / 4)
+                                ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, (g + 1) * REG_TSTRIDE * 16, 0)
+                                : q;
+            if (bits) f(g, q, bits);
+            q = qn;
+        }
+    }
     template <typename F>
     __device__ __forceinline__ void each_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
 #pragma unroll

@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // lane; a bit's kk-th edge is unique, so no two lanes of the
                 // phase write one column), then added and written back by the
                 // lanes whose edge there is a kk-th one.
-                meta.each_group_masked(mlo, mhi, [&](int g, auto q, uint32_t) {
+                meta.each_group_masked_pf(mlo, mhi, [&](int g, auto q, uint32_t) {
                     // the group's four lane masks in one scalar load, before any
                     // LDS access (a scalar-load wait also waits for LDS reads)
                     uint64_t em[4];
