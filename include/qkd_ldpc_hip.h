@@ -163,7 +163,8 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
  * glibc-exact restatement), 4 tanh_lin_approx, 5 atanh_lin_approx
  * (src/qkd_ldpc_algorithm.cpp:146-172), 6 tanh and 7 atanh in the decoder
  * forms the SPA kernel calls, 8 tanh(x / 2.) in the table form of the SPA
- * check-node scan (tanh_half_clip_t; |x| >= 44 gives +-1). */
+ * check-node scan (tanh_half_clip_t; |x| >= 44 gives +-1), 9 clip(2. * atanh(x),
+ * 100) in the SPA message pass's form (atanh2_clip). */
 int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream);
 
 /* Thread-local description of the last failure on this thread. */

@@ -1264,7 +1264,7 @@ int qldpc_keys_match_device(int32_t batch, int32_t n, const uint8_t *d_alice, co
 }
 
 int qldpc_selftest_math_device(int32_t fn, int32_t count, const double *d_in, double *d_out, void *stream) {
-    if (fn < 0 || fn > 8 || count < 0) return fail(QLDPC_EINVAL, "fn must be 0..8, count >= 0");
+    if (fn < 0 || fn > 9 || count < 0) return fail(QLDPC_EINVAL, "fn must be 0..9, count >= 0");
     if (count > 0 && (!d_in || !d_out)) return fail(QLDPC_EINVAL, "NULL device buffer");
     hipError_t e = launch_math_selftest(fn, count, d_in, d_out, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "math_selftest");

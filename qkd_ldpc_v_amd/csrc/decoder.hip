@@ -359,6 +359,9 @@ __global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, c
     int flag = 0;
     switch (fn) {
     case 8: y = ql_exact::tanh_half_clip_t(x, 44.0, 1.0, &flag, ctab); break;  // tanh(clip(x, inf) / 2.), tanh(22) = 1
+    case 9:  // the SPA message pass's clip(2. * atanh(x), 100)
+        y = ql_exact::atanh2_clip(x, 100.0, ql_exact::atanh2_full(0x1.fffffffffffffp-1));
+        break;
     case 0: y = ql_exact::tanh_exact(x); break;
     case 1: y = ql_exact::atanh_exact(x); break;
     case 2: y = ql_exact::expm1_exact(x); break;

@@ -58,7 +58,7 @@ struct V2Layout {
         tail = o;     // (min-sum: a lane's tail aggregate is parked in its row's rowAB entry)
         tailneg = o;
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
-        ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * 16));  // SPA: tanh's expm1 classes
+        ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * sizeof(ql_exact::Expm1Class)));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         bytes = o;
     }

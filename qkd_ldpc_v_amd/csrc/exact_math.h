@@ -665,31 +665,48 @@ QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
 
 // Table form of the per-class constants above.  They depend on k alone, and
 // the common path only reaches k in [-3, 63] (u in (-2, 0] or [2, 44)), so a
-// 67-entry table indexed by k + 3 holds X3, X4 and B (high words; the low
-// words are 0) and the exponent addend k << 20: one 16-byte LDS read replaces
-// the class arithmetic and its selects.  Same constants, same IEEE operations.
+// 67-entry table indexed by k + 3 holds X3, X4 and B and the exponent addend
+// k << 20, and also s_tanh.c's tail constants: |x| >= 1 exactly when k > 0
+// (u >= 2 gives k >= 3, u in (-2, 0] gives k in [-3, 0]), so C and the
+// numerator -2 / -y are class constants too: num = fma(y, NM, NA) with
+// (NM, NA) = (0, -2) or (-1, -0) — y * 0 + -2 == -2 and y * -1 + -0 == -y
+// exactly for finite y (signed zeros included).  The constants are stored as
+// whole doubles (four 16-byte LDS reads land them in register pairs: no
+// assembly of hi words over a zero low word).  Same constants, same IEEE
+// operations as tanh_half_common.
 struct alignas(16) Expm1Class {
-    uint32_t x3_hi, x4_hi, b_hi, k20;
+    double x3, x4, b, c, nm, na;
+    uint32_t k20, pad[3];
 };
 constexpr int EXPM1_K_MIN = -3, EXPM1_K_MAX = 63, EXPM1_CLASSES = EXPM1_K_MAX - EXPM1_K_MIN + 1;
 QL_HD Expm1Class expm1_class(int32_t k) {
     const uint32_t ku = (uint32_t)k;
     const bool fcls = (ku - 20u) <= 36u;
     const bool far = (ku + 1u) > 57u;
+    const bool big = k > 0;
     uint32_t a_hi = 0x3ff00000u - (0x200000u >> (ku & 31u));
     a_hi = (k == 0) ? 0x80000000u : a_hi;
     a_hi = (k == -1) ? 0xbff00000u : a_hi;
     Expm1Class c;
-    c.x3_hi = fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u;
-    c.x4_hi = fcls ? 0x3ff00000u : a_hi;
-    c.b_hi = far ? 0xbff00000u : 0x80000000u;
+    c.x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
+    c.x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
+    c.b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
+    c.c = big ? 1.0 : -0.0;
+    c.nm = big ? 0.0 : -1.0;
+    c.na = big ? -2.0 : -0.0;
     c.k20 = ku << 20;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0;
     return c;
 }
 
 // tanh_half_common with the class constants from `tab` (EXPM1_CLASSES
 // entries, tab[i] = expm1_class(i + EXPM1_K_MIN)).  Lanes outside the common
 // path (the callers' rare branch recomputes them) read a clamped entry.
+// k: s_expm1.c's explicit k = -1 for 0.5 ln2 < |u| < 1.5 ln2 (hi-word tests)
+// is what the rounded formula gives there anyway — only u < 0 reaches that
+// range, where invln2 * u - 0.5 lies in [-1.99999997, -1.00000001] — so only
+// the k = 0 test (|u| <= 0.5 ln2 by hi word) remains.  The result's sign:
+// the magnitude C + num / (y + 2) is > 0 on this path, so copysign by b.
 QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *tab) {
     const double ln2_hi = 6.93147180369123816490e-01;
     const double ln2_lo = 1.90821492927058770002e-10;
@@ -700,7 +717,6 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
 
     const uint32_t jb = hi_word(b);
     const uint32_t ib = jb & 0x7fffffffu;
-    const uint32_t sx = jb & 0x80000000u;
     const bool big = ib >= 0x40000000u;
     const double ab = __builtin_fabs(b);
     const double u = big ? ab : -ab;
@@ -708,7 +724,7 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
 #if !defined(__HIP_DEVICE_COMPILE__)
     kf = (kf > 1e6 || kf < -1e6 || kf != kf) ? 0.0 : kf;
 #endif
-    int32_t k = (ib < 0x3FF0A2B2u) ? -1 : (int32_t)kf;
+    int32_t k = (int32_t)kf;
     k = (ib > 0x3fd62e42u) ? k : 0;
     const int32_t kc = k < EXPM1_K_MIN ? EXPM1_K_MIN : (k > EXPM1_K_MAX ? EXPM1_K_MAX : k);
     const Expm1Class cl = tab[kc - EXPM1_K_MIN];  // issued early, used after the division
@@ -728,19 +744,15 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     const double t3 = 3.0 - r1 * hfx;
     const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
     const double e2 = (xr * (e - c) - c) - hxs;
-    const double X3 = from_words(cl.x3_hi, 0u);
-    const double X4 = from_words(cl.x4_hi, 0u);
-    const double B = from_words(cl.b_hi, 0u);
-    const double ypre = (xr - (e2 + X3)) + X4;
-    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + B;
+    const double ypre = (xr - (e2 + cl.x3)) + cl.x4;
+    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + cl.b;
     // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
     // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
     // end (round-to-nearest is symmetric; the sum is never 0 on this path).
-    const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
-    const double C = from_words(big ? 0x3ff00000u : 0x80000000u, 0u);
-    const double zp = C + div_rn_safe(num, y + 2.0);
+    const double num = __builtin_fma(y, cl.nm, cl.na);
+    const double zp = cl.c + div_rn_safe(num, y + 2.0);
     *ib_out = ib;
-    return from_words(hi_word(zp) ^ sx, lo_word(zp));
+    return __builtin_copysign(zp, b);
 }
 
 QL_HD double tanh_half_dec(double b) {
@@ -806,24 +818,24 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
 
     const double xa = __builtin_fabs(p);
     const uint32_t ia = hi_word(xa);
-    const bool smallx = ia < 0x3fe00000u;          // |p| < 0.5
+    const bool smallx = xa < 0.5;                  // (e_atanh.c: hi word < 0x3fe00000)
     const double twoxa = xa + xa;
     const double qd = div_rn_safe(smallx ? twoxa * xa : twoxa, 1.0 - xa);
     const double a = smallx ? twoxa + qd : qd;
     // --- log1p(a) core, a in [2^-27, 2^22) ---
     const bool k0 = hi_word(a) < 0x3FDA827Au;      // a < 0.41422: f = a, k = 0, c = 0
     const double u0 = 1.0 + a;
-    int32_t hu = (int32_t)hi_word(u0);
-    int32_t k = (hu >> 20) - 1023;                 // >= 0
-    const double cn = (k > 0) ? 1.0 - (u0 - a) : a - (u0 - 1.0);
+    const int32_t hu = (int32_t)hi_word(u0);
+    const double cn = (hu >= 0x3ff00000 + (1 << 20)) ? 1.0 - (u0 - a) : a - (u0 - 1.0);  // k > 0 (u0 >= 2)
     double c = div_rn_safe(cn, u0);
     const uint32_t hm = (uint32_t)hu & 0x000fffffu;
-    const bool up = hm >= 0x6a09eu;
+    // k0 lanes keep k = 0: u0 = 1 + a is in [1, 2) there, so (hu >> 20) - 1023
+    // is 0 and only `up` (possible for a just below 0.41422) must be masked off
+    const bool up = !k0 && hm >= 0x6a09eu;
     const double u = with_hi_word(u0, hm | (up ? 0x3fe00000u : 0x3ff00000u));
-    k = up ? k + 1 : k;
+    const int32_t k = (hu >> 20) - 1023 + (int32_t)up;
     double f = u - 1.0;
     f = k0 ? a : f;
-    k = k0 ? 0 : k;
     c = k0 ? 0.0 : c;
     const double hfsq = 0.5 * f * f;
     const double dk = (double)k;
@@ -874,10 +886,12 @@ QL_HD double atanh2_clip(double p, double thr, double c_top) {
     uint32_t ia;
     double r = atanh2_common(p, &ia);
     const double xa = __builtin_fabs(p);
-    const bool special = (ia < 0x3e300000u) || !(xa < 0x1.fffffffffffffp-1);  // tiny, >= 1 - 2^-53, NaN
+    // (tests on |p| itself: the hi-word test ia < 0x3e300000 is |p| < 2^-28)
+    const bool tiny = xa < 0x1p-28;
+    const bool special = tiny || !(xa < 0x1.fffffffffffffp-1);  // tiny, >= 1 - 2^-53, NaN
     QL_RARE(special || __builtin_fabs(r) > thr) {
         double v = (xa == 1.0) ? __builtin_copysign(__builtin_inf(), p) : __builtin_copysign(c_top, p);
-        v = (ia < 0x3e300000u) ? 2. * p : v;
+        v = tiny ? 2. * p : v;
         v = (xa > 1.0 || p != p) ? 2. * ((p - p) / (p - p)) : v;
         r = clip_thr(special ? v : r, thr);
     }

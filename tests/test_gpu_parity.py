@@ -83,13 +83,14 @@ def test_device_exact_math_bitwise(gpu_available):
     d_in = torch.from_numpy(xs).cuda()
     d_out = torch.empty_like(d_in)
     for fn, name in ((0, "tanh"), (1, "atanh"), (2, "expm1"), (3, "log1p"), (6, "tanh_dec"), (7, "atanh_dec"),
-                     (8, "tanh_half_clip_t")):
+                     (8, "tanh_half_clip_t"), (9, "atanh2_clip")):
         Q._lib.check(Q.lib().qldpc_selftest_math_device(fn, xs.size, d_in.data_ptr(), d_out.data_ptr(), None),
                      "selftest")
         torch.cuda.synchronize()
         got = d_out.cpu().numpy()
         f = {0: math.tanh, 1: math.atanh, 2: math.expm1, 3: math.log1p, 6: math.tanh, 7: math.atanh,
-             8: lambda v: math.tanh(v / 2.)}[fn]  # 8: the SPA scan's table form of tanh(b2c / 2.)
+             8: lambda v: math.tanh(v / 2.),  # 8: the SPA scan's table form of tanh(b2c / 2.)
+             9: lambda v: v if v != v else max(-100.0, min(100.0, 2. * math.atanh(v)))}[fn]  # 9: clipped 2 atanh
 
         def ref(x):
             try:
@@ -97,11 +98,13 @@ def test_device_exact_math_bitwise(gpu_available):
             except (ValueError, OverflowError):
                 if fn in (1, 7):
                     return math.copysign(math.inf, x) if abs(x) == 1 else math.nan
+                if fn == 9:
+                    return math.copysign(100.0, x) if abs(x) == 1 else math.nan
                 if fn == 3:
                     return -math.inf if x == -1 else math.nan
                 return math.inf
         want = np.array([ref(float(x)) for x in xs])
-        assert bits_equal_nan(got, want), f"{name}: {int((got.view(np.uint64) != want.view(np.uint64)).sum())} diffs"
+        assert bits_equal_nan(got, want), f"{name}: {int((~((got == want) | (np.isnan(got) & np.isnan(want)))).sum())} diffs"
 
 
 def test_kat_johnson_on_gpu(gpu_available):

@@ -166,6 +166,28 @@ int main(int argc, char **argv) {
         printf("power-of-two atanh mismatches: %ld\n", pb);
         bb += pb;
     }
+    // log1p arguments a around s_log1p.c's k = 0 cut (hi word 0x3FDA827A) and
+    // the sqrt(2) normalisation cut of u0 = 1 + a (hi word 0x3FF6A09E): for a
+    // just below the k = 0 cut, 1 + a already normalises upwards
+    {
+        const double C_TOP = 2. * std::atanh(0x1.fffffffffffffp-1);
+        long kb = 0;
+        uint64_t s = 99;
+        for (long i = 0; i < 4000000; ++i) {
+            const uint64_t hi = 0x3FDA8270ull + (sm64(s) % 0x14);  // 0x3FDA8270 .. 0x3FDA8283
+            const uint64_t bits = (hi << 32) | (sm64(s) & 0xffffffffull);
+            double a; memcpy(&a, &bits, 8);
+            double pv = a / (a + 2.0);
+            const int e = (int)(sm64(s) % 5) - 2;
+            for (int t = 0; t < (e < 0 ? -e : e); ++t) pv = std::nextafter(pv, e < 0 ? 0.0 : 2.0);
+            const double v = (i & 1) ? -pv : pv;
+            nb += 1;
+            if (!same(ql_exact::atanh2_clip(v, HUGE_VAL, C_TOP), 2. * std::atanh(v)) && kb++ < 5)
+                printf("k0-cut atanh2_clip p=%a ref=%a got=%a\n", v, 2. * std::atanh(v), ql_exact::atanh2_clip(v, HUGE_VAL, C_TOP));
+        }
+        printf("k0-cut atanh mismatches: %ld\n", kb);
+        bb += kb;
+    }
     printf("boundary mismatches: %ld / %ld\n", bb, nb);
     return (tot || bb) ? 1 : 0;
 }
