@@ -92,6 +92,8 @@ struct DeviceGraph {
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
     uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
+    uint64_t *row_sem = nullptr;    // V2 SPA scan: [wave][slot][2] START / END lane masks
+    uint64_t *row_rmask = nullptr;  // V2 SPA scan: [row j][lane] slots of the lane's j-th started row
     std::mutex mu;     // workspaces (ws), occupancy cache
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
@@ -157,6 +159,7 @@ struct qldpc_graph {
     std::vector<int> layout_row_ptr;        // V2: row_ptr of the rows in layout order
     int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
     int hd_uniform_dv = 0;                  // > 0: the staged bits are 0..n-1 in order, all of this degree
+    int nst_max = 0;                        // V2 SPA scan: most rows started in one lane (row_rmask rows)
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
     std::vector<int> part_row0;             // V2 split: first layout row of each part (+ m)
@@ -608,8 +611,17 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
     }
     const bool vng_h = !vng_meta2.empty();
+    // SPA scan row structure (V2, CSR order): per wave and slot the lanes whose
+    // slot starts / ends a row (lane masks the scan tests as scalar registers),
+    // and per lane the slot mask of each row it starts (bit 63: the row
+    // continues into the next lane) for the row parities of the decisions.
+    std::vector<uint64_t> row_sem, row_rmask;
+    int nst_max = 0;
     auto build_meta = [&](bool sorted, std::vector<uint32_t> &mt, std::vector<uint64_t> &vnm,
                           std::vector<uint32_t> &mt2, std::vector<uint64_t> &vex) -> int {
+        const bool rowstruct = v2 && !sorted && g->split_k <= 1 && g->v2RG == 0 && S4 <= 63;
+        std::vector<std::vector<uint64_t>> rm(rowstruct ? T : 0);
+        if (rowstruct) row_sem.assign((size_t)W * S4 * 2, 0);
         mt.assign((size_t)G4 * TS * 4 * NPARTS, 0);
         mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 * NPARTS : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
@@ -658,8 +670,20 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         if (e == lrp[j]) {
                             wd |= META_START;
                             ++lnst[l];
+                            if (rowstruct) {
+                                row_sem[((size_t)w * S4 + k) * 2] |= 1ull << li;
+                                // slots of this row in the lane; bit 63 when it runs past the lane
+                                const long long last = std::min<long long>(lrp[j + 1] - 1, e0 + epl_w - 1);
+                                uint64_t msk = 0;
+                                for (long long q = e; q <= last; ++q) msk |= 1ull << (q - e0);
+                                if (lrp[j + 1] - 1 > e0 + epl_w - 1) msk |= 1ull << 63;
+                                rm[l].push_back(msk);
+                            }
                         }
-                        if (e == lrp[j + 1] - 1 && !(v2 && k < head)) wd |= META_END;
+                        if (e == lrp[j + 1] - 1 && !(v2 && k < head)) {
+                            wd |= META_END;
+                            if (rowstruct) row_sem[((size_t)w * S4 + k) * 2 + 1] |= 1ull << li;
+                        }
                         if (k > 0 && j != prev_row && j != prev_row + 1)
                             return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
                         prev_row = j;
@@ -667,6 +691,12 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                     mt[midx(l, k)] = wd;
                 }
             }
+        }
+        if (rowstruct) {
+            for (auto &v : rm) nst_max = std::max(nst_max, (int)v.size());
+            row_rmask.assign((size_t)std::max(nst_max, 1) * T, 0);
+            for (int l = 0; l < T; ++l)
+                for (size_t j = 0; j < rm[l].size(); ++j) row_rmask[j * T + l] = rm[l][j];
         }
         return QLDPC_OK;
     };
@@ -677,6 +707,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     int brc = build_meta(false, meta, vnm, meta2, vex);
     if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms, meta2_ms, vex_ms);
     if (brc) return brc;
+    g->nst_max = row_sem.empty() ? 0 : nst_max;
     if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
         auto visited = [&](const std::vector<uint64_t> &v) {
             long long s = 0;
@@ -733,7 +764,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso)) ||
             (rc = upload(&dg->vn_rows, vn_rows)) || (rc = upload(&dg->vng_bits, vng_bits)) ||
-            (rc = upload(&dg->vng_meta2, vng_meta2))) {
+            (rc = upload(&dg->vng_meta2, vng_meta2)) || (rc = upload(&dg->row_sem, row_sem)) ||
+            (rc = upload(&dg->row_rmask, row_rmask))) {
             (void)hipSetDevice(prev);
             return rc;
         }
@@ -905,6 +937,9 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
     a.row_orig = dg->row_orig;
+    a.row_sem = (v2 && alg < 2 && g->nst_max > 0) ? dg->row_sem : nullptr;
+    a.row_rmask = (v2 && alg < 2 && g->nst_max > 0) ? dg->row_rmask : nullptr;
+    a.nst_max = g->nst_max;
     a.split_k = v2 ? g->split_k : 1;
     if (v2 && g->split_k > 1) {
         const int slots = (int)w->split_frames + 64;
@@ -1090,6 +1125,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->vn_rows);
         (void)hipFree(d->vng_bits);
         (void)hipFree(d->vng_meta2);
+        (void)hipFree(d->row_sem);
+        (void)hipFree(d->row_rmask);
         for (auto &kv : d->ws) {
             (void)hipFree(kv.second.counter);
             (void)hipFree(kv.second.scratch);

@@ -183,6 +183,9 @@ struct MetaSrc {
         }
     }
 };
+// Read-only for a kernel's lifetime: loads through this type are scalar (s_load).
+typedef const __attribute__((address_space(4))) uint64_t cu64_t;
+
 // Issue priority of a SIMD's waves, rotated slot group by slot group: the
 // sequencer otherwise favours the oldest wave, so a SIMD's four waves finish a
 // phase one after another and the last runs alone (one wave cannot issue

@@ -27,6 +27,11 @@ namespace {
 using namespace dev;
 
 constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
+#ifdef QL_NO_ROWSCAN
+constexpr bool V2_ROWSCAN_ON = false;  // A/B only: SPA scan with per-slot flag bookkeeping
+#else
+constexpr bool V2_ROWSCAN_ON = true;
+#endif
 
 __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -47,8 +52,9 @@ constexpr int V2_A0_ENTRIES = 64;
 // memory and the palette indices are read from the 2-bit global codes; LDS
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
-    size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, bytes;
-    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0) {
+    size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, syn, bytes;
+    __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0,
+                                 bool rowscan = false) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
@@ -60,6 +66,18 @@ struct V2Layout {
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
         ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * sizeof(ql_exact::Expm1Class)));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
+        // SPA, one workgroup per frame: the rows' target syndrome bits as sign
+        // words (s << 31), in the palette-index area past the codes when it has room
+        syn = 0;
+        if (rowscan && !minsum && !split) {
+            const size_t cs = V2_CODES_OFF + al16((size_t)n);
+            if (cs + (size_t)m * 4 <= (size_t)V2_CODES_OFF + V2_CODES_CAP) {
+                syn = cs;
+            } else {
+                syn = o;
+                o = al16(o + (size_t)m * 4);
+            }
+        }
         bytes = o;
     }
 };
@@ -76,17 +94,17 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 // SPLIT: a frame is decoded by a.split_k workgroups of one XCD (planner
 // parts: contiguous blocks of 16 waves' rows), which meet at every phase
 // boundary through a global arrival counter; totals are in global memory.
-template <bool SPLIT, int RL, bool RGLB>
+template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true);
-    else return V2Layout(a.n, RGLB ? 0 : a.m, a.nc, a.T, minsum, false, RL);
+    else return V2Layout(a.n, RGLB ? 0 : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
 // Whether a launch runs the LDS-slot instantiation (RL = V2_RL): SPA family,
 // register shape V2_R_TIGHT, and the frame's LDS image plus the slots fit.
 __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, int n, int m, int T) {
     if (alg > 1 || R != V2_R_TIGHT || RG != 0 || split || T > REG_TSTRIDE) return false;
-    return V2Layout(n, m, (n + 3) / 4, T, false, false, V2_RL).bytes <= 160 * 1024;
+    return V2Layout(n, m, (n + 3) / 4, T, false, false, V2_RL, V2_ROWSCAN_ON).bytes <= 160 * 1024;
 }
 
 constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
@@ -137,6 +155,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // hybrid bit gather: per-slot padded edge positions in slot_meta2
     constexpr bool VNG_H = VNG && RG > 0;
     constexpr int KT = v2_tail_slots<S>();
+    // SPA family on one-workgroup register frames: the scan takes the row
+    // structure from scalar lane masks (a.row_sem) and the row parities from
+    // a per-lane decision bit vector (a.row_rmask) instead of per-slot flag
+    // bookkeeping; row products are unsigned until their END, where the
+    // syndrome sign goes on (sign flips commute with round-to-nearest).
+    constexpr bool ROWSCAN = V2_ROWSCAN_ON && SPA_FAM && !SPLIT && RG == 0;
 
     const int tid = threadIdx.x;
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
@@ -144,7 +168,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const double thr = a.thr_on ? a.thr : __builtin_inf();
     const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
     static_assert(!RGLB || (VNG && RG > 0), "rows in global scratch: hybrid bit gather only");
-    const V2Layout L = v2_layout<SPLIT, RL, RGLB>(a, !SPA_FAM);
+    const V2Layout L = v2_layout<SPLIT, RL, RGLB, ROWSCAN>(a, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
     int *s_part = reinterpret_cast<int *>(smem) + 2;  // SPLIT: rank, sync slot
@@ -323,6 +347,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 codes4[i] = (b & 3u) | (((b >> 2) & 3u) << 8) | (((b >> 4) & 3u) << 16) | ((b >> 6) << 24);
             }
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
+            if constexpr (ROWSCAN) {
+                uint32_t *syn = reinterpret_cast<uint32_t *>(smem + L.syn);
+                for (int r = tid; r < m; r += T) syn[r] = (uint32_t)(sy[a.row_orig[r]] & 1) << 31;
+            }
         }
         STAMP(ST_SETUP);
         __syncthreads();
@@ -689,8 +717,81 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             // (set only on rows begun in this lane) publishes it.  Slots before
             // the first START are the tail of the previous lane's last row.
             int r = row0;
-            int par = 0, cur_s = 0, mis = 0, neg = 0, big = 0;
+            int mis = 0, big = 0;
             int div_unsafe = 0;
+            if constexpr (ROWSCAN) {
+                // Decisions z_k = (total <= 0) are shifted into zA (slots 0..31)
+                // and zB (32..), one v_addc per slot; a row's parity is then the
+                // popcount of z under the row's slot mask, after the loop.
+                uint32_t zA = 0, zB = 0;
+                double acc = 1.0;
+                const uint32_t *syn = reinterpret_cast<const uint32_t *>(smem + L.syn);
+                const cu64_t *sem = (const cu64_t *)(a.row_sem + (size_t)wave * S * 2);
+                // slot k's {START, END} masks are loaded during slot k - 1, after
+                // that slot's LDS read is consumed (SMEM and LDS share one wait
+                // counter: a scalar load in flight would hold up the LDS wait)
+                uint64_t smk = sem[0], emk = sem[1];
+                meta.each_upto(epl, [&](int k, uint32_t mt) {
+                    const double tv = total[(int)(mt & META_COL_MASK)];
+                    double b;
+                    if constexpr (ALG == 0) b = tv - c2b.get(k);  // b2c = total - c2b (:115); +0 in iteration 0
+                    else b = clip_msg(tv - c2b.get(k), thr_it);    // (:115, :122-123; :21-29)
+                    asm volatile("" ::"v"(b) : "memory");
+                    const uint64_t smk_n = (k + 1 < S) ? sem[2 * k + 2] : 0, emk_n = (k + 1 < S) ? sem[2 * k + 3] : 0;
+                    const bool start = __builtin_amdgcn_inverse_ballot_w64(smk);
+                    if (k > 0) r += start ? 1 : 0;
+                    const uint32_t sv = syn[r];  // sign word of the row this slot belongs to
+                    const uint32_t zb = (tv <= 0.0) ? 1u : 0u;
+                    if (k < 32) zA = zA + zA + zb;
+                    else zB = zB + zB + zb;
+                    double t = b;
+                    if constexpr (ALG == 0) {
+                        if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // (:60)
+                    } else {
+                        if (compute) t = tanh_lin(b / 2.);
+                    }
+                    c2b.set(k, t);
+                    // running product in CSR order (:57-62), unsigned: the row's
+                    // sign (s ? -1 : 1) is applied at its END
+                    acc = (start ? 1.0 : acc) * t;
+                    if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
+                        rowA[r] = ql_exact::with_hi_word(acc, ql_exact::hi_word(acc) ^ sv);
+                        if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
+                    }
+                    smk = smk_n;
+                    emk = emk_n;
+                });
+                // bit k of (zlo, zhi) = decision of slot k
+                const int na = epl < 32 ? epl : 32;
+                const uint32_t zlo = __builtin_bitreverse32(zA) >> (32 - na);
+                const uint32_t zhi = (epl > 32) ? (__builtin_bitreverse32(zB) >> (64 - epl)) : 0u;
+                // rows started in this lane: parity of the decisions under the
+                // row's slots vs its target syndrome bit (sm: bit j = j-th START)
+                int popen = 0;
+                for (int j = 0; j < a.nst_max; ++j) {
+                    if (j < nst) {
+                        const uint64_t mk = a.row_rmask[(size_t)j * T + tid];
+                        const int p = (__builtin_popcount(zlo & (uint32_t)mk) +
+                                       __builtin_popcount(zhi & (uint32_t)(mk >> 32) & 0x7fffffffu)) & 1;
+                        if (mk >> 63) popen = p;  // continues in the next lane
+                        else mis |= p ^ (int)((sm >> j) & 1u);
+                    }
+                }
+                // a row split across two lanes of this wave: finished here
+                const int ppar = __shfl(popen, up, 64);
+                const int hpar = __builtin_popcount(zlo & ((1u << head) - 1u)) & 1;
+                const double pacc = __shfl(acc, up, 64);
+                if (head > 0) {
+                    double p = pacc;  // continue the row's product in CSR order
+#pragma unroll
+                    for (int k = 0; k < KT; ++k)
+                        if (k < head) p = p * c2b.get(k);
+                    rowA[row0] = ql_exact::with_hi_word(p, ql_exact::hi_word(p) ^ syn[row0]);
+                    if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(p) >= 0x1p-900) ? 0 : 1;
+                    mis |= ppar ^ hpar ^ s_row0;
+                }
+            } else {
+            int par = 0, cur_s = 0, neg = 0;
             uint32_t zt = 0;  // decisions of the first KT slots (tail parity)
             double acc = 1.0, m1 = DBL_MAX, m2 = DBL_MAX;
             auto scan_slot = [&](int k, uint32_t mt, double tv) {
@@ -789,6 +890,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     }
                 }
             }
+            }  // !ROWSCAN
             if constexpr (SPLIT) {
                 if (mis) __hip_atomic_store(gmis, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -1000,7 +1102,8 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, bool rows_global) {
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
-    return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0).bytes;
+    return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
+                    V2_ROWSCAN_ON && alg < 2 && !split && RG == 0).bytes;
 }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
@@ -1010,6 +1113,8 @@ bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
+    // the SPA-family scan of one-workgroup register frames reads the row structure masks
+    if (a.alg < 2 && a.split_k <= 1 && a.v2RG == 0 && !a.row_sem) return hipErrorInvalidValue;
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)

@@ -674,9 +674,17 @@ QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
 // whole doubles (four 16-byte LDS reads land them in register pairs: no
 // assembly of hi words over a zero low word).  Same constants, same IEEE
 // operations as tanh_half_common.
+#ifndef QL_CTAB
+#define QL_CTAB 32  // entry bytes: 32 (B and C as high words: fewer live registers) or 64 (all doubles)
+#endif
 struct alignas(16) Expm1Class {
+#if QL_CTAB == 64
     double x3, x4, b, c, nm, na;
     uint32_t k20, pad[3];
+#else
+    double x3, x4;
+    uint32_t b_hi, c_hi, k20, pad;
+#endif
 };
 constexpr int EXPM1_K_MIN = -3, EXPM1_K_MAX = 63, EXPM1_CLASSES = EXPM1_K_MAX - EXPM1_K_MIN + 1;
 QL_HD Expm1Class expm1_class(int32_t k) {
@@ -690,12 +698,19 @@ QL_HD Expm1Class expm1_class(int32_t k) {
     Expm1Class c;
     c.x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
     c.x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
+#if QL_CTAB == 64
     c.b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
     c.c = big ? 1.0 : -0.0;
     c.nm = big ? 0.0 : -1.0;
     c.na = big ? -2.0 : -0.0;
     c.k20 = ku << 20;
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
+#else
+    c.b_hi = far ? 0xbff00000u : 0x80000000u;
+    c.c_hi = big ? 0x3ff00000u : 0x80000000u;
+    c.k20 = ku << 20;
+    c.pad = 0;
+#endif
     return c;
 }
 
@@ -745,12 +760,18 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
     const double e2 = (xr * (e - c) - c) - hxs;
     const double ypre = (xr - (e2 + cl.x3)) + cl.x4;
-    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + cl.b;
     // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
     // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
     // end (round-to-nearest is symmetric; the sum is never 0 on this path).
+#if QL_CTAB == 64
+    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + cl.b;
     const double num = __builtin_fma(y, cl.nm, cl.na);
     const double zp = cl.c + div_rn_safe(num, y + 2.0);
+#else
+    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + from_words(cl.b_hi, 0u);
+    const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
+    const double zp = from_words(cl.c_hi, 0u) + div_rn_safe(num, y + 2.0);
+#endif
     *ib_out = ib;
     return __builtin_copysign(zp, b);
 }
@@ -826,15 +847,19 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     const bool k0 = hi_word(a) < 0x3FDA827Au;      // a < 0.41422: f = a, k = 0, c = 0
     const double u0 = 1.0 + a;
     const int32_t hu = (int32_t)hi_word(u0);
-    const double cn = (hu >= 0x3ff00000 + (1 << 20)) ? 1.0 - (u0 - a) : a - (u0 - 1.0);  // k > 0 (u0 >= 2)
-    double c = div_rn_safe(cn, u0);
+    // c = the rounding error of 1 + a, divided by u0.  s_log1p.c forms it as
+    // 1 - (u0 - a) when u0 >= 2 and a - (u0 - 1) otherwise; on a in [2^-27,
+    // 2^22) both differences of each form are exact (Sterbenz; u0 - 1 is a
+    // multiple of ulp(u0) below 2^53), so both forms are the same exact
+    // value and one of them serves every lane.
+    double c = div_rn_safe(a - (u0 - 1.0), u0);
     const uint32_t hm = (uint32_t)hu & 0x000fffffu;
     // k0 lanes keep k = 0: u0 = 1 + a is in [1, 2) there, so (hu >> 20) - 1023
     // is 0 and only `up` (possible for a just below 0.41422) must be masked off
     const bool up = !k0 && hm >= 0x6a09eu;
-    const double u = with_hi_word(u0, hm | (up ? 0x3fe00000u : 0x3ff00000u));
     const int32_t k = (hu >> 20) - 1023 + (int32_t)up;
-    double f = u - 1.0;
+    // u = u0 with its exponent replaced (SET_HIGH_WORD) = u0 * 2^-k exactly
+    double f = __builtin_ldexp(u0, -k) - 1.0;
     f = k0 ? a : f;
     c = k0 ? 0.0 : c;
     const double hfsq = 0.5 * f * f;
@@ -855,7 +880,7 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     // hm) >> 2 : hm), i.e. !k0 && (hm == 0 || hm >= 0xffffd): one test on hm
     // admits exactly those four values (k0 lanes included), the exact
     // condition is applied inside.
-    QL_RARE(((hm + 3u) & 0xfffffu) < 4u) {
+    QL_RARE(((uint32_t)hu << 12) + 0x3000u < 0x4000u) {  // ((hm + 3) mod 2^20) < 4
         const uint32_t hu2 = k0 ? 1u : (up ? (0x00100000u - hm) >> 2 : hm);
         if (hu2 == 0) {                            // |f| < 2^-20
             const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
