@@ -468,37 +468,35 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
                 const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
                 const const_u64 *ex = vn_exec + (size_t)kk * S;
-                // Four slots at a time: the four totals are read together (every
-                // lane; a bit's kk-th edge is unique, so no two lanes of the
-                // phase write one column), then added and written back by the
-                // lanes whose edge there is a kk-th one.
-                meta.each_group_masked_pf(mlo, mhi, [&](int g, auto q, uint32_t) {
-                    // the group's four lane masks in one scalar load, before any
-                    // LDS access (a scalar-load wait also waits for LDS reads)
-                    uint64_t em[4];
+                // Eight slots (two groups) at a time: their totals are read
+                // together by the lanes whose edge there is a kk-th one (a bit's
+                // kk-th edge is unique: no two slots of the phase touch one
+                // column), then added and written back — one LDS round trip per
+                // pair of groups.
+                meta.each_group_pair_masked_pf(mlo, mhi, [&](int g, auto qa, auto qb, bool two) {
+                    // the lane masks by scalar loads, before any LDS access (a
+                    // scalar-load wait also waits for LDS reads)
+                    uint64_t em[8];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) em[i] = ex[4 * g + i];
-                    double tv[4];
-#ifdef QL_VN_UNMASKED_READS
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
-#else
-                    // only the lanes whose edge there is a kk-th one read (a
-                    // quarter of them on a dv = 4 code): LDS bytes and bank
-                    // conflicts of the phase drop with the lanes
+                    for (int i = 0; i < 8; ++i) em[i] = (i < 4 || two) ? ex[4 * g + i] : 0ull;
+                    uint32_t cl[8];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
+                        cl[i] = (uint32_t)qa[i] & META_COL_MASK;
+                        cl[4 + i] = (uint32_t)qb[i] & META_COL_MASK;
+                    }
+                    double tv[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
                         // (inactive lanes' tv is never used: the add below runs
                         // under the same mask)
                         asm("" : "=v"(tv[i]));
-                        if (__builtin_amdgcn_inverse_ballot_w64(em[i]))
-                            tv[i] = total[(int)((uint32_t)q[i] & META_COL_MASK)];
+                        if ((i < 4 || two) && __builtin_amdgcn_inverse_ballot_w64(em[i])) tv[i] = total[(int)cl[i]];
                     }
-#endif
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (__builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
-                            total[(int)((uint32_t)q[i] & META_COL_MASK)] = tv[i] + c2b.get(4 * g + i);
+                    for (int i = 0; i < 8; ++i)
+                        if ((i < 4 || two) && __builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
+                            total[(int)cl[i]] = tv[i] + c2b.get((4 * g + i) < S ? 4 * g + i : 0);
                 });
                 STAMP(ST_VNK);
                 psync();
