@@ -307,26 +307,35 @@ struct MetaSrcW : MetaSrc<R> {
             q = qn;
         }
     }
-    // Pairs of groups (g, g + 1) at least one of which is in the mask:
-    // f(g, q_g, q_g+1, two) — two: group g + 1 exists.  The next pair's first
-    // group's metadata is requested before this pair's work.
-    template <typename F>
-    __device__ __forceinline__ void each_group_pair_masked_pf(uint32_t mlo, uint32_t mhi, F &&f) const {
-        auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
+    // Batches of NB consecutive groups at least one of which is in the mask:
+    // f(g, q[NB], nv) — q[j] the metadata of group g + j, nv the groups that
+    // exist.  The next batch's first group's metadata is requested before
+    // this batch's work.
+    template <int NB, typename F>
+    __device__ __forceinline__ void each_group_batch_masked_pf(uint32_t mlo, uint32_t mhi, F &&f) const {
+        constexpr int NG = R / 4;
+        auto q0 = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
 #pragma unroll
-        for (int g = 0; g < R / 4; g += 2) {
-            constexpr int NG = R / 4;
-            const bool two = g + 1 < NG;
-            const uint32_t w0 = (4 * g < 32) ? mlo : mhi;
-            const uint32_t w1 = (4 * (g + 1) < 32) ? mlo : mhi;
-            const uint32_t bits = ((w0 >> ((4 * g) & 31)) & 15u) | (two ? ((w1 >> ((4 * (g + 1)) & 31)) & 15u) : 0u);
-            const auto qb = two ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, (g + 1) * REG_TSTRIDE * 16, 0)
-                                : q;
-            const auto qn = (g + 2 < NG)
-                                ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, (g + 2) * REG_TSTRIDE * 16, 0)
-                                : q;
-            if (bits) f(g, q, qb, two);
-            q = qn;
+        for (int g = 0; g < NG; g += NB) {
+            uint32_t bits = 0;
+            decltype(q0) q[NB];
+            q[0] = q0;
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                if (g + j < NG) {
+                    const uint32_t w = (4 * (g + j) < 32) ? mlo : mhi;
+                    bits |= (w >> ((4 * (g + j)) & 31)) & 15u;
+                    if (j > 0)
+                        q[j] = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, (g + j) * REG_TSTRIDE * 16, 0);
+                } else {
+                    q[j] = q0;
+                }
+            }
+            const auto qn = (g + NB < NG)
+                                ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, (g + NB) * REG_TSTRIDE * 16, 0)
+                                : q0;
+            if (bits) f(g, q, (NG - g < NB) ? NG - g : NB);
+            q0 = qn;
         }
     }
     template <typename F>

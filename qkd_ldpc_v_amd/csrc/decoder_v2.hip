@@ -27,6 +27,10 @@ namespace {
 using namespace dev;
 
 constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
+#ifndef QL_VN_BATCH
+#define QL_VN_BATCH 2
+#endif
+constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS round trip
 #ifdef QL_NO_ROWSCAN
 constexpr bool V2_ROWSCAN_ON = false;  // A/B only: SPA scan with per-slot flag bookkeeping
 #else
@@ -468,35 +472,32 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 const uint32_t mlo = __builtin_amdgcn_readfirstlane((uint32_t)vm);
                 const uint32_t mhi = __builtin_amdgcn_readfirstlane((uint32_t)(vm >> 32));
                 const const_u64 *ex = vn_exec + (size_t)kk * S;
-                // Eight slots (two groups) at a time: their totals are read
-                // together by the lanes whose edge there is a kk-th one (a bit's
-                // kk-th edge is unique: no two slots of the phase touch one
-                // column), then added and written back — one LDS round trip per
-                // pair of groups.
-                meta.each_group_pair_masked_pf(mlo, mhi, [&](int g, auto qa, auto qb, bool two) {
+                // V2_VN_BATCH groups of four slots at a time: their totals are
+                // read together by the lanes whose edge there is a kk-th one (a
+                // bit's kk-th edge is unique: no two slots of the phase touch
+                // one column), then added and written back — one LDS round trip
+                // per batch.
+                meta.template each_group_batch_masked_pf<V2_VN_BATCH>(mlo, mhi, [&](int g, auto q, int nv) {
+                    constexpr int NS = 4 * V2_VN_BATCH;
                     // the lane masks by scalar loads, before any LDS access (a
                     // scalar-load wait also waits for LDS reads)
-                    uint64_t em[8];
+                    uint64_t em[NS];
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) em[i] = (i < 4 || two) ? ex[4 * g + i] : 0ull;
-                    uint32_t cl[8];
+                    for (int i = 0; i < NS; ++i) em[i] = (i < 4 * nv) ? ex[4 * g + i] : 0ull;
+                    double tv[NS];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        cl[i] = (uint32_t)qa[i] & META_COL_MASK;
-                        cl[4 + i] = (uint32_t)qb[i] & META_COL_MASK;
-                    }
-                    double tv[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
+                    for (int i = 0; i < NS; ++i) {
                         // (inactive lanes' tv is never used: the add below runs
                         // under the same mask)
                         asm("" : "=v"(tv[i]));
-                        if ((i < 4 || two) && __builtin_amdgcn_inverse_ballot_w64(em[i])) tv[i] = total[(int)cl[i]];
+                        if (i < 4 * nv && __builtin_amdgcn_inverse_ballot_w64(em[i]))
+                            tv[i] = total[(int)((uint32_t)q[i / 4][i % 4] & META_COL_MASK)];
                     }
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        if ((i < 4 || two) && __builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
-                            total[(int)cl[i]] = tv[i] + c2b.get((4 * g + i) < S ? 4 * g + i : 0);
+                    for (int i = 0; i < NS; ++i)
+                        if (i < 4 * nv && __builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
+                            total[(int)((uint32_t)q[i / 4][i % 4] & META_COL_MASK)] =
+                                tv[i] + c2b.get((4 * g + i) < S ? 4 * g + i : 0);
                 });
                 STAMP(ST_VNK);
                 psync();
