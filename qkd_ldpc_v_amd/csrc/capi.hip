@@ -92,8 +92,8 @@ struct DeviceGraph {
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
     uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
-    uint64_t *row_sem = nullptr;    // V2 SPA scan: [wave][slot][2] START / END lane masks
-    uint64_t *row_rmask = nullptr;  // V2 SPA scan: [row j][lane] slots of the lane's j-th started row
+    uint64_t *row_sem = nullptr;    // V2 scan: [wave][slot][4] START / END / PARK lane masks (+ pad)
+    uint64_t *row_rmask = nullptr;  // V2 scan: [row j][lane] slots of the lane's j-th started row
     std::mutex mu;     // workspaces (ws), occupancy cache
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
@@ -611,8 +611,10 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
     }
     const bool vng_h = !vng_meta2.empty();
-    // SPA scan row structure (V2, CSR order): per wave and slot the lanes whose
-    // slot starts / ends a row (lane masks the scan tests as scalar registers),
+    // Scan row structure (V2; row boundaries are the same in the CSR and the
+    // kpos-sorted layout): per wave and slot the lanes whose slot starts / ends
+    // a row, and (min-sum) parks its tail aggregate (lane masks the scan tests
+    // as scalar registers),
     // and per lane the slot mask of each row it starts (bit 63: the row
     // continues into the next lane) for the row parities of the decisions.
     std::vector<uint64_t> row_sem, row_rmask;
@@ -621,7 +623,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                           std::vector<uint32_t> &mt2, std::vector<uint64_t> &vex) -> int {
         const bool rowstruct = v2 && !sorted && g->split_k <= 1 && g->v2RG == 0 && S4 <= 63;
         std::vector<std::vector<uint64_t>> rm(rowstruct ? T : 0);
-        if (rowstruct) row_sem.assign((size_t)W * S4 * 2, 0);
+        if (rowstruct) row_sem.assign((size_t)W * S4 * 4, 0);
         mt.assign((size_t)G4 * TS * 4 * NPARTS, 0);
         mt2.assign(g->n_hd ? (size_t)G4 * TS * 4 * NPARTS : 0, 0);
         vnm.assign(v2 ? (size_t)W * g->dv_max : 0, 0);
@@ -671,7 +673,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                             wd |= META_START;
                             ++lnst[l];
                             if (rowstruct) {
-                                row_sem[((size_t)w * S4 + k) * 2] |= 1ull << li;
+                                row_sem[((size_t)w * S4 + k) * 4] |= 1ull << li;
                                 // slots of this row in the lane; bit 63 when it runs past the lane
                                 const long long last = std::min<long long>(lrp[j + 1] - 1, e0 + epl_w - 1);
                                 uint64_t msk = 0;
@@ -682,13 +684,18 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         }
                         if (e == lrp[j + 1] - 1 && !(v2 && k < head)) {
                             wd |= META_END;
-                            if (rowstruct) row_sem[((size_t)w * S4 + k) * 2 + 1] |= 1ull << li;
+                            if (rowstruct) row_sem[((size_t)w * S4 + k) * 4 + 1] |= 1ull << li;
                         }
                         if (k > 0 && j != prev_row && j != prev_row + 1)
                             return fail(QLDPC_EUNSUP, "empty check rows between non-empty rows are not supported");
                         prev_row = j;
                     }
                     mt[midx(l, k)] = wd;
+                    // min-sum: a lane's tail aggregate (a row begun in the lane
+                    // before) is parked at slot `head` — its first START, or a
+                    // dummy slot when the wave's edges end with the tail
+                    if (rowstruct && head > 0 && k == head && k < S4)
+                        row_sem[((size_t)w * S4 + k) * 4 + 2] |= 1ull << li;
                 }
             }
         }
@@ -937,8 +944,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
     a.row_orig = dg->row_orig;
-    a.row_sem = (v2 && alg < 2 && g->nst_max > 0) ? dg->row_sem : nullptr;
-    a.row_rmask = (v2 && alg < 2 && g->nst_max > 0) ? dg->row_rmask : nullptr;
+    a.row_sem = (v2 && g->nst_max > 0) ? dg->row_sem : nullptr;
+    a.row_rmask = (v2 && g->nst_max > 0) ? dg->row_rmask : nullptr;
     a.nst_max = g->nst_max;
     a.split_k = v2 ? g->split_k : 1;
     if (v2 && g->split_k > 1) {

@@ -101,10 +101,9 @@ struct DecodeArgs {
     const uint32_t *slot_meta2;     // like slot_meta: stage index of the slot's edge
     long long stage_wg_offset;      // doubles from a workgroup's scratch base to its stage
     const int32_t *row_orig;        // V2: layout row -> original row (syndrome index)
-    // V2 SPA-family scan (one workgroup per frame, register slots only): the
-    // row structure as lane masks and per-lane row slot masks (capi.hip);
-    // null: the scan tracks rows from the metadata flags instead
-    const uint64_t *row_sem;        // [waves][slots][2]: the lanes whose slot starts / ends a row
+    // V2 scan (one workgroup per frame, register slots only): the row
+    // structure as lane masks and per-lane row slot masks (capi.hip)
+    const uint64_t *row_sem;        // [waves][slots][4]: the lanes whose slot starts / ends a row / parks a tail
     const uint64_t *row_rmask;      // [nst_max][T]: slots of the lane's j-th started row; bit 63: open
     int nst_max;
     // V2 split frames (split_k > 1 workgroups of one XCD per frame)

@@ -70,10 +70,10 @@ struct V2Layout {
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
         ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * sizeof(ql_exact::Expm1Class)));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
-        // SPA, one workgroup per frame: the rows' target syndrome bits as sign
-        // words (s << 31), in the palette-index area past the codes when it has room
+        // one workgroup per frame: the rows' target syndrome bits as sign words
+        // (s << 31), in the palette-index area past the codes when it has room
         syn = 0;
-        if (rowscan && !minsum && !split) {
+        if (rowscan && !split) {
             const size_t cs = V2_CODES_OFF + al16((size_t)n);
             if (cs + (size_t)m * 4 <= (size_t)V2_CODES_OFF + V2_CODES_CAP) {
                 syn = cs;
@@ -159,12 +159,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // hybrid bit gather: per-slot padded edge positions in slot_meta2
     constexpr bool VNG_H = VNG && RG > 0;
     constexpr int KT = v2_tail_slots<S>();
-    // SPA family on one-workgroup register frames: the scan takes the row
-    // structure from scalar lane masks (a.row_sem) and the row parities from
-    // a per-lane decision bit vector (a.row_rmask) instead of per-slot flag
-    // bookkeeping; row products are unsigned until their END, where the
-    // syndrome sign goes on (sign flips commute with round-to-nearest).
-    constexpr bool ROWSCAN = V2_ROWSCAN_ON && SPA_FAM && !SPLIT && RG == 0;
+    // One-workgroup register frames: the scan takes the row structure from
+    // scalar lane masks (a.row_sem) and the row parities from a per-lane
+    // decision bit vector (a.row_rmask) instead of per-slot flag bookkeeping;
+    // SPA row products are unsigned until their END, where the syndrome sign
+    // goes on (sign flips commute with round-to-nearest); min-sum rows get
+    // their sign at END and (ANMSA/AOMSA) their mismatch flag after the loop.
+    constexpr bool ROWSCAN = V2_ROWSCAN_ON && !SPLIT && RG == 0;
 
     const int tid = threadIdx.x;
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
@@ -351,10 +352,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 codes4[i] = (b & 3u) | (((b >> 2) & 3u) << 8) | (((b >> 4) & 3u) << 16) | ((b >> 6) << 24);
             }
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
-            if constexpr (ROWSCAN) {
-                uint32_t *syn = reinterpret_cast<uint32_t *>(smem + L.syn);
-                for (int r = tid; r < m; r += T) syn[r] = (uint32_t)(sy[a.row_orig[r]] & 1) << 31;
-            }
+        }
+        if constexpr (ROWSCAN) {  // the rows' target syndrome bits as sign words
+            uint32_t *syn = reinterpret_cast<uint32_t *>(smem + L.syn);
+            for (int r = tid; r < m; r += T) syn[r] = (uint32_t)(sy[a.row_orig[r]] & 1) << 31;
         }
         STAMP(ST_SETUP);
         __syncthreads();
@@ -720,45 +721,75 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             int div_unsafe = 0;
             if constexpr (ROWSCAN) {
                 // Decisions z_k = (total <= 0) are shifted into zA (slots 0..31)
-                // and zB (32..), one v_addc per slot; a row's parity is then the
+                // and zB (32..), one shift per slot; a row's parity is then the
                 // popcount of z under the row's slot mask, after the loop.
                 uint32_t zA = 0, zB = 0;
-                double acc = 1.0;
+                double acc = 1.0;                      // SPA: running product
+                double m1 = DBL_MAX, m2 = DBL_MAX;     // min-sum: aggregate (:381-397)
+                int neg = 0;
                 const uint32_t *syn = reinterpret_cast<const uint32_t *>(smem + L.syn);
-                const cu64_t *sem = (const cu64_t *)(a.row_sem + (size_t)wave * S * 2);
-                // slot k's {START, END} masks are loaded during slot k - 1, after
-                // that slot's LDS read is consumed (SMEM and LDS share one wait
-                // counter: a scalar load in flight would hold up the LDS wait)
-                uint64_t smk = sem[0], emk = sem[1];
+                const cu64_t *sem = (const cu64_t *)(a.row_sem + (size_t)wave * S * 4);
+                // slot k's {START, END, PARK} masks are loaded during slot k - 1,
+                // after that slot's LDS read is consumed (SMEM and LDS share one
+                // wait counter: a scalar load in flight would hold up the LDS wait)
+                uint64_t smk = sem[0], emk = sem[1], pmk = sem[2];
                 meta.each_upto(epl, [&](int k, uint32_t mt) {
                     const double tv = total[(int)(mt & META_COL_MASK)];
                     double b;
                     if constexpr (ALG == 0) b = tv - c2b.get(k);  // b2c = total - c2b (:115); +0 in iteration 0
                     else b = clip_msg(tv - c2b.get(k), thr_it);    // (:115, :122-123; :21-29)
                     asm volatile("" ::"v"(b) : "memory");
-                    const uint64_t smk_n = (k + 1 < S) ? sem[2 * k + 2] : 0, emk_n = (k + 1 < S) ? sem[2 * k + 3] : 0;
+                    const bool more = k + 1 < S;
+                    const uint64_t smk_n = more ? sem[4 * k + 4] : 0, emk_n = more ? sem[4 * k + 5] : 0;
+                    const uint64_t pmk_n = (!SPA_FAM && more) ? sem[4 * k + 6] : 0;
                     const bool start = __builtin_amdgcn_inverse_ballot_w64(smk);
                     if (k > 0) r += start ? 1 : 0;
                     const uint32_t sv = syn[r];  // sign word of the row this slot belongs to
                     const uint32_t zb = (tv <= 0.0) ? 1u : 0u;
                     if (k < 32) zA = zA + zA + zb;
                     else zB = zB + zB + zb;
-                    double t = b;
-                    if constexpr (ALG == 0) {
-                        if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // (:60)
+                    if constexpr (SPA_FAM) {
+                        double t = b;
+                        if constexpr (ALG == 0) {
+                            if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // (:60)
+                        } else {
+                            if (compute) t = tanh_lin(b / 2.);
+                        }
+                        c2b.set(k, t);
+                        // running product in CSR order (:57-62), unsigned: the
+                        // row's sign (s ? -1 : 1) is applied at its END
+                        acc = (start ? 1.0 : acc) * t;
+                        if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
+                            rowA[r] = ql_exact::with_hi_word(acc, ql_exact::hi_word(acc) ^ sv);
+                            if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
+                        }
                     } else {
-                        if (compute) t = tanh_lin(b / 2.);
-                    }
-                    c2b.set(k, t);
-                    // running product in CSR order (:57-62), unsigned: the row's
-                    // sign (s ? -1 : 1) is applied at its END
-                    acc = (start ? 1.0 : acc) * t;
-                    if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
-                        rowA[r] = ql_exact::with_hi_word(acc, ql_exact::hi_word(acc) ^ sv);
-                        if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
+                        const double x = b;
+                        c2b.set(k, x);
+                        // the first START closes the tail segment of a row begun in
+                        // the lane before: its aggregate (parity of negatives in
+                        // min1's sign bit) is parked in that row's own entry
+                        if (k > 0 && k < KT && __builtin_amdgcn_inverse_ballot_w64(pmk))
+                            rowAB[row0] = ms_pack(m1, m2, neg, 0);
+                        m1 = start ? DBL_MAX : m1;
+                        m2 = start ? DBL_MAX : m2;
+                        neg = start ? 0 : neg;
+                        // agg_push (:381-397), branch-free
+                        neg ^= (x < 0) ? 1 : 0;
+                        const double ax = __builtin_fabs(x);
+                        const bool lt1 = ax < m1, lt2 = ax < m2;
+                        m2 = lt1 ? m1 : (lt2 ? ax : m2);
+                        m1 = lt1 ? ax : m1;
+                        if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
+                            // s xor parity(negatives) in min1's sign; the mismatch
+                            // flag (ANMSA/AOMSA) is set after the loop
+                            rowAB[r] = ms_pack(m1, m2, neg ^ (int)(sv >> 31), 0);
+                            big |= (m2 > thr) ? 1 : 0;
+                        }
                     }
                     smk = smk_n;
                     emk = emk_n;
+                    pmk = pmk_n;
                 });
                 // bit k of (zlo, zhi) = decision of slot k
                 const int na = epl < 32 ? epl : 32;
@@ -767,27 +798,54 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // rows started in this lane: parity of the decisions under the
                 // row's slots vs its target syndrome bit (sm: bit j = j-th START)
                 int popen = 0;
+                const int rs0 = row0 + (head > 0 ? 1 : 0);
                 for (int j = 0; j < a.nst_max; ++j) {
                     if (j < nst) {
                         const uint64_t mk = a.row_rmask[(size_t)j * T + tid];
                         const int p = (__builtin_popcount(zlo & (uint32_t)mk) +
                                        __builtin_popcount(zhi & (uint32_t)(mk >> 32) & 0x7fffffffu)) & 1;
-                        if (mk >> 63) popen = p;  // continues in the next lane
-                        else mis |= p ^ (int)((sm >> j) & 1u);
+                        if (mk >> 63) {
+                            popen = p;  // continues in the next lane
+                        } else {
+                            const int mr = p ^ (int)((sm >> j) & 1u);
+                            mis |= mr;
+                            if constexpr (ADAPT) {  // factor selector in min2's sign bit (:749-757)
+                                if (mr) reinterpret_cast<uint32_t *>(rowAB + rs0 + j)[3] |= 0x80000000u;
+                            }
+                        }
                     }
                 }
                 // a row split across two lanes of this wave: finished here
                 const int ppar = __shfl(popen, up, 64);
                 const int hpar = __builtin_popcount(zlo & ((1u << head) - 1u)) & 1;
-                const double pacc = __shfl(acc, up, 64);
-                if (head > 0) {
-                    double p = pacc;  // continue the row's product in CSR order
+                if constexpr (SPA_FAM) {
+                    const double pacc = __shfl(acc, up, 64);
+                    if (head > 0) {
+                        double p = pacc;  // continue the row's product in CSR order
 #pragma unroll
-                    for (int k = 0; k < KT; ++k)
-                        if (k < head) p = p * c2b.get(k);
-                    rowA[row0] = ql_exact::with_hi_word(p, ql_exact::hi_word(p) ^ syn[row0]);
-                    if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(p) >= 0x1p-900) ? 0 : 1;
-                    mis |= ppar ^ hpar ^ s_row0;
+                        for (int k = 0; k < KT; ++k)
+                            if (k < head) p = p * c2b.get(k);
+                        rowA[row0] = ql_exact::with_hi_word(p, ql_exact::hi_word(p) ^ syn[row0]);
+                        if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(p) >= 0x1p-900) ? 0 : 1;
+                        mis |= ppar ^ hpar ^ s_row0;
+                    }
+                } else {
+                    MinAgg t;
+                    t.m1 = __shfl(m1, up, 64);
+                    t.m2 = __shfl(m2, up, 64);
+                    t.neg = __shfl(neg, up, 64);
+                    if (head > 0) {
+                        const double2 ta = rowAB[row0];
+                        MinAgg h;
+                        h.m1 = __builtin_fabs(ta.x);
+                        h.m2 = ta.y;
+                        h.neg = (int)(ql_exact::hi_word(ta.x) >> 31);
+                        agg_merge(t, h);
+                        const int mr = ppar ^ hpar ^ s_row0;
+                        rowAB[row0] = ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr);
+                        big |= (t.m2 > thr) ? 1 : 0;
+                        mis |= mr;
+                    }
                 }
             } else {
             int par = 0, cur_s = 0, neg = 0;
@@ -1102,7 +1160,7 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, bool rows_global) {
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
     return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
-                    V2_ROWSCAN_ON && alg < 2 && !split && RG == 0).bytes;
+                    V2_ROWSCAN_ON && !split && RG == 0).bytes;
 }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
@@ -1112,8 +1170,8 @@ bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
 }
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
-    // the SPA-family scan of one-workgroup register frames reads the row structure masks
-    if (a.alg < 2 && a.split_k <= 1 && a.v2RG == 0 && !a.row_sem) return hipErrorInvalidValue;
+    // the scan of one-workgroup register frames reads the row structure masks
+    if (a.split_k <= 1 && a.v2RG == 0 && !a.row_sem) return hipErrorInvalidValue;
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
