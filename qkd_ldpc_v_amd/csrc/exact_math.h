@@ -857,13 +857,13 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     // k0 lanes keep k = 0: u0 = 1 + a is in [1, 2) there, so (hu >> 20) - 1023
     // is 0 and only `up` (possible for a just below 0.41422) must be masked off
     const bool up = !k0 && hm >= 0x6a09eu;
-    const int32_t k = (hu >> 20) - 1023 + (int32_t)up;
+    const int32_t nk = 1023 - (hu >> 20) - (int32_t)up;  // -k
     // u = u0 with its exponent replaced (SET_HIGH_WORD) = u0 * 2^-k exactly
-    double f = __builtin_ldexp(u0, -k) - 1.0;
+    double f = __builtin_ldexp(u0, nk) - 1.0;
     f = k0 ? a : f;
     c = k0 ? 0.0 : c;
     const double hfsq = 0.5 * f * f;
-    const double dk = (double)k;
+    const double ndk = (double)nk;  // -k: the k products below by negation (RN is symmetric)
     const double s = div_rn_safe(f, 2.0 + f);
     const double z = s * s;
     const double R1 = z * Lp1;
@@ -874,14 +874,19 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     const double z6 = z4 * z2;
     const double R4 = Lp6 + z * Lp7;
     const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
-    // k == 0 through the k != 0 formula (dk = c = 0): see atanh_dec
-    double y = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
+    // k == 0 through the k != 0 formula (dk = c = 0): see atanh_dec.
+    // dk * ln2_hi == -(ndk * ln2_hi) and dk * ln2_lo + c == c - ndk * ln2_lo
+    // bitwise; k == 0 only on k0 lanes, where the sum is never 0, so the
+    // -0 of -(0 * ln2_hi) cannot surface.
+    double y = -(ndk * ln2_hi) - ((hfsq - (s * (hfsq + R) + (c - ndk * ln2_lo))) - f);
     // s_log1p.c's |f| < 2^-20 case is hu == 0 with hu = k0 ? 1 : (up ? (0x100000 -
     // hm) >> 2 : hm), i.e. !k0 && (hm == 0 || hm >= 0xffffd): one test on hm
     // admits exactly those four values (k0 lanes included), the exact
     // condition is applied inside.
-    QL_RARE(((uint32_t)hu << 12) + 0x3000u < 0x4000u) {  // ((hm + 3) mod 2^20) < 4
+    QL_RARE((((uint32_t)hu + 3u) << 12) < 0x4000u) {  // ((hm + 3) mod 2^20) < 4
         const uint32_t hu2 = k0 ? 1u : (up ? (0x00100000u - hm) >> 2 : hm);
+        const int32_t k = -nk;
+        const double dk = (double)k;
         if (hu2 == 0) {                            // |f| < 2^-20
             const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
             const double ysmall = (k == 0) ? f - Rs : dk * ln2_hi - ((Rs - (dk * ln2_lo + c)) - f);
