@@ -100,7 +100,7 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 // boundary through a global arrival counter; totals are in global memory.
 template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
-    if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true);
+    if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL);
     else return V2Layout(a.n, RGLB ? 0 : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
@@ -109,6 +109,14 @@ __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) 
 __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, int n, int m, int T) {
     if (alg > 1 || R != V2_R_TIGHT || RG != 0 || split || T > REG_TSTRIDE) return false;
     return V2Layout(n, m, (n + 3) / 4, T, false, false, V2_RL, V2_ROWSCAN_ON).bytes <= 160 * 1024;
+}
+// Split frames keep their totals in global memory, so a part's LDS holds only
+// its rows: the SPA family keeps V2_RL_SPLIT of the 40 message slots there
+// (the register kernel otherwise spills in its slot loops).  m: the largest
+// part's row count.
+constexpr int V2_RL_SPLIT = 12;
+__host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows) {
+    return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, REG_TSTRIDE, false, true, V2_RL_SPLIT).bytes <= 160 * 1024;
 }
 
 constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
@@ -1147,7 +1155,11 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
 }
 
 KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
-    if (split_k > 1) return pick_v2<V2_R_TIGHT, 0, true>(alg);
+    if (split_k > 1) {
+        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT>
+                                : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT>;
+        return pick_v2<V2_R_TIGHT, 0, true>(alg);
+    }
     if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, false, V2_RL> : decode_v2_kernel<1, V2_R_TIGHT, 0, false, V2_RL>;
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
     if (R == V2_R_TIGHT) return pick_v2<V2_R_TIGHT, 0>(alg);
@@ -1158,6 +1170,7 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 }  // namespace
 
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, bool rows_global) {
+    if (split) return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m) ? V2_RL_SPLIT : 0).bytes;
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
     return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
                     V2_ROWSCAN_ON && !split && RG == 0).bytes;
@@ -1176,7 +1189,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
-                                       v2_use_rl(a.alg, a.v2R, a.v2RG, a.split_k > 1, a.n, a.m, a.T));
+                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows)
+                                                     : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
