@@ -114,7 +114,10 @@ __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, in
 // its rows: the SPA family keeps V2_RL_SPLIT of the 40 message slots there
 // (the register kernel otherwise spills in its slot loops).  m: the largest
 // part's row count.
-constexpr int V2_RL_SPLIT = 12;
+#ifndef QL_RL_SPLIT
+#define QL_RL_SPLIT 12
+#endif
+constexpr int V2_RL_SPLIT = QL_RL_SPLIT;
 __host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows) {
     return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, REG_TSTRIDE, false, true, V2_RL_SPLIT).bytes <= 160 * 1024;
 }
