@@ -744,7 +744,7 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     const int32_t kc = k < EXPM1_K_MIN ? EXPM1_K_MIN : (k > EXPM1_K_MAX ? EXPM1_K_MAX : k);
     const Expm1Class cl = tab[kc - EXPM1_K_MIN];  // issued early, used after the division
     const double t = (double)k;
-    const double hi = u - t * ln2_hi;
+    const double hi = __builtin_fma(-t, ln2_hi, u);  // == u - t * ln2_hi: t * ln2_hi is exact (ln2_hi has 32 bits, |k| < 2^11)
     const double lo = t * ln2_lo;
     const double xr = hi - lo;
     const double c = (hi - xr) - lo;
@@ -878,7 +878,7 @@ QL_HD double atanh2_common(double p, uint32_t *ia_out) {
     // dk * ln2_hi == -(ndk * ln2_hi) and dk * ln2_lo + c == c - ndk * ln2_lo
     // bitwise; k == 0 only on k0 lanes, where the sum is never 0, so the
     // -0 of -(0 * ln2_hi) cannot surface.
-    double y = -(ndk * ln2_hi) - ((hfsq - (s * (hfsq + R) + (c - ndk * ln2_lo))) - f);
+    double y = __builtin_fma(-ndk, ln2_hi, -((hfsq - (s * (hfsq + R) + (c - ndk * ln2_lo))) - f));  // ndk * ln2_hi is exact
     // s_log1p.c's |f| < 2^-20 case is hu == 0 with hu = k0 ? 1 : (up ? (0x100000 -
     // hm) >> 2 : hm), i.e. !k0 && (hm == 0 || hm >= 0xffffd): one test on hm
     // admits exactly those four values (k0 lanes included), the exact
