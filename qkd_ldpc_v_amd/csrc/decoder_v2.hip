@@ -564,14 +564,24 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // terms read row 0 and are not added).
                 auto gather_r = [&](auto dct) {
                     constexpr bool DC = decltype(dct)::value;
-                    const uint2 *vr = a.vn_rows;
+                    // buffer loads with 32-bit offsets (descriptors in SGPRs): no
+                    // 64-bit address arithmetic per bit
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    const __amdgpu_buffer_rsrc_t vr_rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)a.vn_rows, (short)0, n * 8, 0x00020000);
+                    const __amdgpu_buffer_rsrc_t gc_rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)gcodes, (short)0, paletted ? nc : 0, 0x00020000);
+                    auto ld_rows = [&](int bb) -> uint2 {
+                        const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(vr_rs, bb * 8, 0, 0));
+                        return make_uint2(v.x, v.y);
+                    };
                     int b = tid;
                     uint2 rr = make_uint2(0u, 0u);
                     uint32_t gcn = 0;
                     double lrn = 0.0;
                     if (b < n) {
-                        rr = vr[b];
-                        if (paletted) gcn = gcodes[b >> 2];
+                        rr = ld_rows(b);
+                        if (paletted) gcn = __builtin_amdgcn_raw_buffer_load_b8(gc_rs, b >> 2, 0, 0);
                         else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, b * 8, 0, 0));
                     }
                     for (; b < n; b += T) {
@@ -580,8 +590,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         const double lr = lrn;
                         const int bn = b + T;
                         if (bn < n) {
-                            rr = vr[bn];
-                            if (paletted) gcn = gcodes[bn >> 2];
+                            rr = ld_rows(bn);
+                            if (paletted) gcn = __builtin_amdgcn_raw_buffer_load_b8(gc_rs, bn >> 2, 0, 0);
                             else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, bn * 8, 0, 0));
                         }
                         const uint32_t cb = codes[b];
