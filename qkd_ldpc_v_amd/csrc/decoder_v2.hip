@@ -371,9 +371,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         STAMP(ST_SETUP);
         __syncthreads();
         STAMP(ST_SETUP_WAIT);
+        // the frame's 2-bit channel codes by byte buffer loads (32-bit offsets)
+        const __amdgpu_buffer_rsrc_t gcodes_rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)gcodes, (short)0, paletted ? nc : 0, 0x00020000);
         auto llr_of = [&](int col) -> double {
             if constexpr (SPLIT || VNG) {
-                if (paletted) return pal[(gcodes[col >> 2] >> ((col & 3) * 2)) & 3];
+                if (paletted)
+                    return pal[((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(gcodes_rs, col >> 2, 0, 0) >> ((col & 3) * 2)) & 3];
             } else {
                 if (paletted) return pal[codes[col]];
             }
@@ -524,18 +528,27 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // uniform msclip picks one by a scalar branch)
                 auto gather_h = [&](auto dct) {
                     constexpr bool DC = decltype(dct)::value;
-                    const uint2 *vr = a.vn_rows;
+                    // buffer loads with 32-bit offsets (descriptors in SGPRs)
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    const __amdgpu_buffer_rsrc_t vr_rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)a.vn_rows, (short)0, 0x7fffffff, 0x00020000);
+                    const __amdgpu_buffer_rsrc_t vb_rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)a.vng_bits, (short)0, n * 8, 0x00020000);
+                    auto ld2 = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off) -> uint2 {
+                        const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0));
+                        return make_uint2(v.x, v.y);
+                    };
                     for (int i = tid; i < n; i += T) {
-                        const uint2 e = a.vng_bits[i];
+                        const uint2 e = ld2(vb_rs, (uint32_t)i * 8u);
                         const int b = (int)e.x;
                         const uint32_t c0 = e.y & 0xFFFFFFu;
                         const int dvb = (int)(e.y >> 24);
                         double sacc = llr_of(b);
-                        uint2 rr = vr[c0];
+                        uint2 rr = ld2(vr_rs, c0 * 8u);
                         for (int kc = 0; kc < dvb; kc += 4) {
                             const uint32_t ch = c0 + (uint32_t)(kc >> 2);
                             const uint2 cur = rr;
-                            if (kc + 4 < dvb) rr = vr[ch + 1];
+                            if (kc + 4 < dvb) rr = ld2(vr_rs, (ch + 1) * 8u);
                             const uint32_t cb = codes[ch];
                             codes[ch] = 0;
                             double2 ab[4];
