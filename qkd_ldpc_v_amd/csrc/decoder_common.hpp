@@ -183,6 +183,19 @@ struct MetaSrc {
         }
     }
 };
+// a + b + (this lane's bit of the lane mask m): one v_addc with the mask as
+// carry-in (the compiler otherwise materialises the bit: a select and an add).
+__device__ __forceinline__ uint32_t add_carry(uint32_t a, uint32_t b, uint64_t m) {
+    uint32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(co) : "v"(a), "v"(b), "s"(m));
+    (void)co;
+    return r;
+}
+__device__ __forceinline__ int add_carry(int a, int b, uint64_t m) {
+    return (int)add_carry((uint32_t)a, (uint32_t)b, m);
+}
+
 // Read-only for a kernel's lifetime: loads through this type are scalar (s_load).
 typedef const __attribute__((address_space(4))) uint64_t cu64_t;
 

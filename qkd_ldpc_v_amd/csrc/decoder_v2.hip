@@ -777,11 +777,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const uint64_t smk_n = more ? sem[4 * k + 4] : 0, emk_n = more ? sem[4 * k + 5] : 0;
                     const uint64_t pmk_n = (!SPA_FAM && more) ? sem[4 * k + 6] : 0;
                     const bool start = __builtin_amdgcn_inverse_ballot_w64(smk);
-                    if (k > 0) r += start ? 1 : 0;
+                    if (k > 0) r = add_carry(r, 0, smk);  // r += START
                     const uint32_t sv = syn[r];  // sign word of the row this slot belongs to
-                    const uint32_t zb = (tv <= 0.0) ? 1u : 0u;
-                    if (k < 32) zA = zA + zA + zb;
-                    else zB = zB + zB + zb;
+                    // z = z * 2 + (total <= 0): the compare's lane mask is the carry-in
+                    const uint64_t zm = __builtin_amdgcn_ballot_w64(tv <= 0.0);
+                    if (k < 32) zA = add_carry(zA, zA, zm);
+                    else zB = add_carry(zB, zB, zm);
                     if constexpr (SPA_FAM) {
                         double t = b;
                         if constexpr (ALG == 0) {
@@ -794,8 +795,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // row's sign (s ? -1 : 1) is applied at its END
                         acc = (start ? 1.0 : acc) * t;
                         if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
-                            rowA[r] = ql_exact::with_hi_word(acc, ql_exact::hi_word(acc) ^ sv);
-                            if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
+                            // two word stores: the low word straight from acc's register
+                            uint32_t *ra = reinterpret_cast<uint32_t *>(rowA + r);
+                            ra[0] = ql_exact::lo_word(acc);
+                            ra[1] = ql_exact::hi_word(acc) ^ sv;
+                            if constexpr (ALG == 0) {
+                                if (!(__builtin_fabs(acc) >= 0x1p-900)) div_unsafe = 1;
+                            }
                         }
                     } else {
                         const double x = b;
