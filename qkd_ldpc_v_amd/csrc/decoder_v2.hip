@@ -1017,8 +1017,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 
             // ---- check-to-bit messages + VN phase 0 (total = llr + first message) ----
             r = row0;
+            // SPA on ROWSCAN shapes: the row counter by the scalar START mask
+            // (v_addc; the min-sum message pass is too short to hide the load)
+            const cu64_t *sem_m = ROWSCAN ? (const cu64_t *)(a.row_sem + (size_t)wave * S * 4) : nullptr;
             auto message = [&](int k, uint32_t mt, uint32_t mt2) {
-                if (k > 0) r += (mt & META_START) ? 1 : 0;
+                if constexpr (ROWSCAN && SPA_FAM) {
+                    if (k > 0) r = add_carry(r, 0, sem_m[4 * k]);
+                } else {
+                    if (k > 0) r += (mt & META_START) ? 1 : 0;
+                }
                 double c;
                 if constexpr (ALG == 0) {
                     // 2. * atanh(rp / t) (:66-68) and the clip (:73-74) in one
