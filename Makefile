@@ -7,7 +7,7 @@ CSRC := $(PKG)/csrc
 # -amdgpu-atomic-optimizer-strategy=None: the atomic optimizer rewrites a uniform
 # atomic into a single-lane block (mbcnt + narrowed exec); with this register
 # pressure LLVM (ROCm 7.2) placed a VGPR spill store inside such a block in the
-# split-frame kernel, so 63 lanes reloaded an unwritten slot (DESIGN.md §3.6).
+# split-frame kernel, so 63 lanes reloaded an unwritten slot (DESIGN.md §3.3).
 # Every atomic here is already issued by one lane on purpose.
 HIPFLAGS := --offload-arch=$(ARCH) $(EXTRA_HIPFLAGS) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result \
             -mllvm -amdgpu-atomic-optimizer-strategy=None
