@@ -92,6 +92,7 @@ struct DeviceGraph {
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
     uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
+    uint32_t *vng_rec = nullptr;  // register-shape bit gather: per slot, the code word's byte offset | shift << 16
     uint64_t *row_sem = nullptr;    // V2 scan: [wave][slot][4] START / END / PARK lane masks (+ pad)
     uint64_t *row_rmask = nullptr;  // V2 scan: [row j][lane] slots of the lane's j-th started row
     std::mutex mu;     // workspaces (ws), occupancy cache
@@ -611,6 +612,11 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
     }
     const bool vng_h = !vng_meta2.empty();
+    // Register-shape bit gather: per slot where the message pass ORs the
+    // edge's two bits — the byte offset of the bit's code word and the
+    // shift of its kpos-th bit pair (8 (col & 3) + 2 kpos).
+    std::vector<uint32_t> vng_rec;
+    if (v2 && !vn_rows.empty() && g->v2RG == 0) vng_rec.assign((size_t)G4 * TS * 4 * NPARTS, 0);
     // Scan row structure (V2; row boundaries are the same in the CSR and the
     // kpos-sorted layout): per wave and slot the lanes whose slot starts / ends
     // a row, and (min-sum) parks its tail aggregate (lane masks the scan tests
@@ -666,6 +672,10 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                             vex[((size_t)w * g->dv_max + kpos[ed]) * S4 + k] |= 1ull << li;
                         }
                         if (sorted && vng_h) vng_meta2[midx(l, k)] = (uint32_t)(P0[col_idx[ed]] + kpos[ed]);
+                        if (sorted && !vng_rec.empty() && kpos[ed] < 4) {
+                            const uint32_t c = (uint32_t)col_idx[ed];
+                            vng_rec[midx(l, k)] = (c & ~3u) | ((((c & 3u) << 3) + 2u * (uint32_t)kpos[ed]) << 16);
+                        }
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
                             mt2[midx(l, k)] =
                                 (uint32_t)(stage_off[kpos[ed]] + rank[col_idx[ed]]);
@@ -772,6 +782,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso)) ||
             (rc = upload(&dg->vn_rows, vn_rows)) || (rc = upload(&dg->vng_bits, vng_bits)) ||
             (rc = upload(&dg->vng_meta2, vng_meta2)) || (rc = upload(&dg->row_sem, row_sem)) ||
+            (rc = upload(&dg->vng_rec, vng_rec)) ||
             (rc = upload(&dg->row_rmask, row_rmask))) {
             (void)hipSetDevice(prev);
             return rc;
@@ -974,6 +985,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
             if (g->v2RG > 0) {
                 a.vng_bits = reinterpret_cast<const uint2 *>(dg->vng_bits);
                 a.slot_meta2 = dg->vng_meta2;
+            } else {
+                a.slot_meta2 = dg->vng_rec;
             }
         }
         if (a.rows_wg_offset >= 0 && !a.vn_rows)
@@ -1132,6 +1145,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->vn_rows);
         (void)hipFree(d->vng_bits);
         (void)hipFree(d->vng_meta2);
+        (void)hipFree(d->vng_rec);
         (void)hipFree(d->row_sem);
         (void)hipFree(d->row_rmask);
         for (auto &kv : d->ws) {

@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     __amdgpu_buffer_rsrc_t stage_rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)stage, (short)0, GATHER ? 0x7fffffff : 0, 0x00020000);
     __amdgpu_buffer_rsrc_t meta2_rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)a.slot_meta2, (short)0, (GATHER || VNG_H) ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
+        (void *)a.slot_meta2, (short)0, (GATHER || VNG) ? S / 4 * REG_TSTRIDE * 16 : 0, 0x00020000);
     const int k0 = GATHER ? a.vn_k0 : (VNG ? 1 : a.dv_max);
     // Per-lane partition constants (capi.hip plan_v2): tail length, first row,
     // rows started here, and the wave's slot count (uniform across the wave).
@@ -1050,12 +1050,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                                               (xneg | (eq1 ? 2u : 0u)) << ((mt2 & 15u) * 2),
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     } else if constexpr (VNG) {
-                        // record the two bits the bit gather rebuilds this message from
+                        // record the two bits the bit gather rebuilds this message
+                        // from, at the word and shift the host precomputed (mt2)
                         const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
                         if (kp < 4u) {  // (dummy slots: kpos META_KPOS_MASK)
-                            const int col = (int)(mt & META_COL_MASK);
-                            __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes) + (col >> 2),
-                                                  (xneg | (eq1 ? 2u : 0u)) << (((col & 3) << 3) + 2 * kp),
+                            __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes + (mt2 & 0xFFFFu)),
+                                                  (xneg | (eq1 ? 2u : 0u)) << (mt2 >> 16),
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     }
@@ -1063,7 +1063,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 emit(k, mt, mt2, c);
             };
-            if constexpr (GATHER || VNG_H) {
+            if constexpr (GATHER || VNG) {
                 meta.each_upto2(epl, meta2_rs, message);
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
