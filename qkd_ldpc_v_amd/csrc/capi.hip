@@ -319,7 +319,9 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         // hybrid shape they may live in global scratch instead when the bit
         // gather applies (then only the SPA image, 8 B/row, must fit)
         bool rows_global = false;
-        if (lds_bytes_v2(2, g.n, g.m, W * 64) > LDS_LIMIT) {
+        // (the shape's own layout: the mask-driven scan's syndrome words exist
+        // on the register shapes only)
+        if (lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1]) > LDS_LIMIT) {
             if (sh[1] == 0 || !g.vng_h_fit || g.m >= 0xFFFF ||
                 lds_bytes_v2(0, g.n, g.m, W * 64, false, sh[0], sh[1]) > LDS_LIMIT ||
                 lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], true) > LDS_LIMIT)
