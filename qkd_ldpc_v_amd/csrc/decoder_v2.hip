@@ -814,8 +814,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         m1 = start ? DBL_MAX : m1;
                         m2 = start ? DBL_MAX : m2;
                         neg = start ? 0 : neg;
-                        // agg_push (:381-397), branch-free
-                        neg ^= (x < 0) ? 1 : 0;
+                        // agg_push (:381-397), branch-free; the count of negatives
+                        // by v_addc (only its parity bit is ever read)
+                        neg = add_carry(neg, 0, __builtin_amdgcn_ballot_w64(x < 0));
                         const double ax = __builtin_fabs(x);
                         const bool lt1 = ax < m1, lt2 = ax < m2;
                         m2 = lt1 ? m1 : (lt2 ? ax : m2);
