@@ -437,19 +437,23 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // (parity of negative b2c) in min1's sign bit and its syndrome
         // mismatch (the adaptive factor's selector) in min2's.
         auto ms_message = [&](double2 ab, uint32_t xneg, bool eq1, bool doclip) -> double {
-            // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all +-1
-            const uint32_t sb = (ql_exact::hi_word(ab.x) >> 31) ^ xneg;
-            const double prod = sb ? -1. : 1.;
+            // sp = (s?-1:1)(-1)^neg (:376,398); prod = sp (x>0?1:-1) (:402): all
+            // +-1, and a product by +-1 is a sign flip that commutes with
+            // round-to-nearest (signed zeros included), so the reference's
+            // fac * prod * sel and prod * max0(d) are computed unsigned and the
+            // sign bit goes on by XOR
+            const uint32_t sgn = (ql_exact::hi_word(ab.x) ^ (xneg << 31)) & 0x80000000u;
             const double sel = eq1 ? __builtin_fabs(ab.y) : __builtin_fabs(ab.x);  // :406
             double fac = a.primary;
             if (ADAPT && (ql_exact::hi_word(ab.y) >> 31)) fac = a.secondary;  // :749-757
             double c;
             if constexpr (NORM) {
-                c = fac * prod * sel;
+                c = fac * sel;
             } else {
                 const double d = sel - fac;
-                c = prod * ((d < 0.) ? 0. : d);
+                c = (d < 0.) ? 0. : d;
             }
+            c = ql_exact::with_hi_word(c, ql_exact::hi_word(c) ^ sgn);
             if (doclip) {  // (:73-74; a no-op otherwise, see msclip)
                 // a real scalar branch on the uniform flag: the empty volatile
                 // asm keeps the compiler from turning the clip into selects
