@@ -426,6 +426,24 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // kept min2 > thr (rows with < 2 non-NaN b2c): flagged by the scan.
         bool msclip = a.thr_on != 0;
         int *s_big = reinterpret_cast<int *>(smem) + 2;  // (non-split only: s_part's slot)
+        // The reference's strict-< two-minimum update (:386-396: ax < m1 ->
+        // (ax, m1); else ax < m2 -> (m1, ax)) as min/max: with 0 <= m1 <= m2
+        // and ax = |x| >= +0 (no signed zeros), the new m2 is the median
+        // max(m1, min(ax, m2)) and the new m1 is min(m1, ax) — ties give
+        // equal values, and a NaN ax leaves both unchanged exactly as the
+        // reference's false compares do (IEEE minNum / maxNum return the
+        // other operand).
+        // (v_min/v_max_f64 directly: no input here is a signalling NaN — ax
+        // comes from arithmetic, m1 / m2 from DBL_MAX and these results — so
+        // the compiler's canonicalising copies for fminnum are dropped)
+        auto ms_push = [](double &m1, double &m2, double ax) {
+            double t, u;
+            asm("v_min_f64 %0, %1, %2" : "=v"(t) : "v"(ax), "v"(m2));
+            asm("v_max_f64 %0, %1, %2" : "=v"(u) : "v"(m1), "v"(t));
+            asm("v_min_f64 %0, %1, %2" : "=v"(t) : "v"(m1), "v"(ax));
+            m2 = u;
+            m1 = t;
+        };
         auto ms_pack = [](double m1, double m2, int sgn, int mr) -> double2 {
             return make_double2(__builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m1) | ((uint64_t)(sgn & 1) << 63)),
                                 __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m2) | ((uint64_t)(mr & 1) << 63)));
@@ -821,10 +839,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // agg_push (:381-397), branch-free; the count of negatives
                         // by v_addc (only its parity bit is ever read)
                         neg = add_carry(neg, 0, __builtin_amdgcn_ballot_w64(x < 0));
-                        const double ax = __builtin_fabs(x);
-                        const bool lt1 = ax < m1, lt2 = ax < m2;
-                        m2 = lt1 ? m1 : (lt2 ? ax : m2);
-                        m1 = lt1 ? ax : m1;
+                        ms_push(m1, m2, __builtin_fabs(x));
                         if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
                             // s xor parity(negatives) in min1's sign; the mismatch
                             // flag (ANMSA/AOMSA) is set after the loop
@@ -932,10 +947,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     neg = start ? 0 : neg;
                     // agg_push (:381-397), branch-free
                     neg ^= (x < 0) ? 1 : 0;
-                    const double ax = __builtin_fabs(x);
-                    const bool lt1 = ax < m1, lt2 = ax < m2;
-                    m2 = lt1 ? m1 : (lt2 ? ax : m2);
-                    m1 = lt1 ? ax : m1;
+                    ms_push(m1, m2, __builtin_fabs(x));
                 }
                 cur_s = start ? s : cur_s;
                 sm = start ? (sm >> 1) : sm;
