@@ -831,11 +831,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // the first START closes the tail segment of a row begun in
                         // the lane before: its aggregate (parity of negatives in
                         // min1's sign bit) is parked in that row's own entry
-                        if (k > 0 && k < KT && __builtin_amdgcn_inverse_ballot_w64(pmk))
+                        // (the aggregate restarts after a row's END and after the
+                        // park — the slot after either is a START — so a START
+                        // needs no selects)
+                        if (k > 0 && k < KT && __builtin_amdgcn_inverse_ballot_w64(pmk)) {
                             rowAB[row0] = ms_pack(m1, m2, neg, 0);
-                        m1 = start ? DBL_MAX : m1;
-                        m2 = start ? DBL_MAX : m2;
-                        neg = start ? 0 : neg;
+                            m1 = DBL_MAX;
+                            m2 = DBL_MAX;
+                            neg = 0;
+                        }
                         // agg_push (:381-397), branch-free; the count of negatives
                         // by v_addc (only its parity bit is ever read)
                         neg = add_carry(neg, 0, __builtin_amdgcn_ballot_w64(x < 0));
@@ -845,6 +849,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                             // flag (ANMSA/AOMSA) is set after the loop
                             rowAB[r] = ms_pack(m1, m2, neg ^ (int)(sv >> 31), 0);
                             big |= (m2 > thr) ? 1 : 0;
+                            m1 = DBL_MAX;
+                            m2 = DBL_MAX;
+                            neg = 0;
                         }
                     }
                     smk = smk_n;
