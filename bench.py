@@ -182,19 +182,18 @@ def main():
     ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
 
-    def step(i, timed=False):
-        sl = slots[i % nst]
-        st = sl.stream
+    def step(i, sl=None):
+        """One batch through the fused per-trial window entry: frame build (LLR
+        palette codes + Alice syndrome) -> decode -> key compare, all enqueued
+        by the library on the slot's stream (no palettize pass: the frame
+        builder writes the decoder's palette form directly)."""
+        sl = sl or slots[i % nst]
         if ra:  # QKD_LDPC_RATE_ADAPT (src/qkd_ldpc_algorithm.cpp:1121-1218)
-            g.build_frames_rate_adapt_device(rplan, ta, tb, pa, pb, tlp, tax, sl.llr_ws, sl.syn_ws, stream=st)
+            g.qkd_ldpc_rate_adapt_device(rplan, params, ta, tb, pa, pb, tlp, tax, sl.llr_ws, sl.syn_ws, sl.bits,
+                                         sl.iters, sl.ok, sl.km, stream=sl.stream)
         else:  # QKD_LDPC (:1031-1087)
-            g.build_frames_device(ta, tb, tlp, sl.llr_ws, sl.syn_ws, stream=st)
-        if timed:
-            ev0[i].record(st)
-        g.decode_device(params, sl.llr_ws, sl.syn_ws, sl.bits, sl.iters, sl.ok, stream=st)
-        if timed:
-            ev1[i].record(st)
-        Q.keys_match_device(tax if ra else ta, sl.bits, sl.km, stream=st)
+            g.qkd_ldpc_device(params, ta, tb, tlp, sl.llr_ws, sl.syn_ws, sl.bits, sl.iters, sl.ok, sl.km,
+                              stream=sl.stream)
 
     log(f"[rank {rank}] {desc}; plan {plan}; warmup {args.warmup}")
     for i in range(args.warmup):
@@ -205,32 +204,35 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i, timed=True)
+        sl = slots[i % nst]
+        ev0[i].record(sl.stream)
+        step(i)
+        ev1[i].record(sl.stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    pipelined_ms = float(np.mean([ev0[i].elapsed_time(ev1[i]) for i in range(args.steps)]))
-    # Roofline: the decode kernel alone — a few serial launches on one stream,
-    # bracketed by HIP events on that stream (outside the timed region).
-    kernel_ms = pipelined_ms
+    step_ms_stream = float(np.mean([ev0[i].elapsed_time(ev1[i]) for i in range(args.steps)]))
+    # Roofline: the decode kernel alone — a few serial steps on one stream with
+    # the library's kernel timing on (HIP events around the decode kernel
+    # launch only, on the stream it runs on), outside the timed region.
+    kernel_ms = None
     if args.roofline_launches > 0:
-        sl = slots[0]
-        r0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.roofline_launches)]
-        r1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.roofline_launches)]
+        g.set_kernel_timing(True)
+        kms = []
         for j in range(args.roofline_launches):
-            r0[j].record(sl.stream)
-            g.decode_device(params, sl.llr_ws, sl.syn_ws, sl.bits, sl.iters, sl.ok, stream=sl.stream)
-            r1[j].record(sl.stream)
-        torch.cuda.synchronize()
-        kernel_ms = float(np.mean([r0[j].elapsed_time(r1[j]) for j in range(args.roofline_launches)]))
+            step(j, slots[0])
+            kms.append(g.last_decode_kernel_ms(slots[0].stream, local))
+        g.set_kernel_timing(False)
+        kernel_ms = float(np.mean(kms))
+        # (the roofline steps decode the same trials as the timed ones)
 
     last = slots[(args.steps - 1) % nst]  # every step decodes the same trials
     it_sum = int(last.iters.to(torch.int64).sum().item())
     n_ok = int(last.ok.to(torch.int64).sum().item())
     n_keys = int(last.km.to(torch.int64).sum().item())
-    tot = combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, batch, kernel_ms, dev)
+    tot = combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, batch, kernel_ms or 0.0, dev)
     elapsed_max, kernel_ms_max = tot["elapsed_max"], tot["kernel_ms_max"]
     it_total, ok_total, keys_total, frames_step = tot["iters"], tot["ok"], tot["keys"], tot["frames"]
 
@@ -238,8 +240,11 @@ def main():
         frames_total = frames_step * args.steps
         value = frames_total * k_info / elapsed_max
         B = 8.0 * (2 * E + 2 * n)  # algorithmic bytes per frame-iteration
-        # per-launch algorithmic bytes of THIS rank's decode kernel / its mean duration
-        achieved = (it_sum * B) / (kernel_ms * 1e-3) / 1e9
+        # per-launch algorithmic bytes of THIS rank's decode kernel / its mean
+        # duration (the serial roofline launches; without them, the timed
+        # steps' per-stream step time, which also holds the frame build)
+        kms = kernel_ms if kernel_ms else step_ms_stream
+        achieved = (it_sum * B) / (kms * 1e-3) / 1e9
         traffic = None
         valu_per_launch = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -278,7 +283,7 @@ def main():
             "mean_iterations": it_total / frames_step,
             "decode_kernel_ms": kernel_ms,
             "decode_kernel_ms_max_rank": kernel_ms_max,
-            "decode_ms_per_step_pipelined": pipelined_ms,
+            "step_ms_per_stream_pipelined": step_ms_stream,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -296,7 +301,7 @@ def main():
             # pass (profiles/pmc_<workload>.json) over this run's kernel time,
             # against the whole-chip VALU issue rate tools/valu_bench.hip
             # measures (profiles/r01/valu_microbench.json).
-            ach = valu_per_launch / (kernel_ms * 1e-3)
+            ach = valu_per_launch / (kms * 1e-3)
             res["compute_roofline"] = {"bound": "fp64-valu-issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR,
                                        "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WAVE_INSTR}
         if world == 1 and not args.no_cpu_baseline:
@@ -329,36 +334,84 @@ def combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, frames, kernel_ms, device
             "ok": float(stats[2]), "keys": float(stats[3]), "frames": float(stats[4])}
 
 
+def host_cpus():
+    """The host CPUs this job may use: nproc (os.cpu_count), the affinity mask,
+    the cgroup CPU quota, and the CPU model (/proc/cpuinfo)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):  # cgroup v2: "<quota> <period>" or "max <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": usable, "model": model}
+
+
 def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info, seed):
     """The CPU oracle (a port of the reference decoder, glibc math, one frame per
     task on a thread pool like src/simulation.cpp:721,740-746) on a bounded
-    sample of the same workload: chunks of frames until `seconds` elapse."""
+    sample of the same workload: chunks of frames until `seconds` elapse, on
+    every host CPU this job may use (value), then on one thread (value_1thread,
+    a third of the time budget)."""
     from oracle import pyoracle as P
     from oracle.pyoracle import Oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cpus = host_cpus()
     O = Oracle(H)
     p = O.params(alg, max_it, True, 100.0, prim, sec)
-    chunk = threads * 4
     seeds = P.trial_seeds(seed, 1 << 16)
-    frames = 0
-    t_dec = 0.0
-    while t_dec < seconds and frames + chunk <= seeds.size:
-        tr = [P.trial(H.n, qber, int(sd)) for sd in seeds[frames:frames + chunk]]  # run_trial's keys, untimed
-        a = np.stack([t[0] for t in tr])
-        b = np.stack([t[1] for t in tr])
-        q = tr[0][2]
-        t0 = time.perf_counter()
-        lp = math.log((1.0 - q) / q)
-        llr = np.where(b != 0, -lp, lp)
-        s = H.syndrome(a)
-        bits, it, ok, _ = O.decode_batch(p, llr, s, threads=threads)
-        (bits == a).all(axis=1)
-        t_dec += time.perf_counter() - t0
-        frames += chunk
-    return {"value": frames * k_info / t_dec, "unit": "info-bits/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} frames of the same workload (chunks of {chunk}), {t_dec:.1f} s, "
-                      f"oracle/ldpc_oracle.c on {threads} host threads"}
+
+    def sample(threads, budget, start):
+        chunk = threads * 4
+        frames, t_dec = 0, 0.0
+        while t_dec < budget and start + frames + chunk <= seeds.size:
+            tr = [P.trial(H.n, qber, int(sd)) for sd in seeds[start + frames:start + frames + chunk]]  # untimed
+            a = np.stack([t[0] for t in tr])
+            b = np.stack([t[1] for t in tr])
+            q = tr[0][2]
+            t0 = time.perf_counter()
+            lp = math.log((1.0 - q) / q)
+            llr = np.where(b != 0, -lp, lp)
+            s = H.syndrome(a)
+            bits, it, ok, _ = O.decode_batch(p, llr, s, threads=threads)
+            (bits == a).all(axis=1)
+            t_dec += time.perf_counter() - t0
+            frames += chunk
+        return frames, t_dec
+
+    threads = cpus["usable"]
+    frames, t_all = sample(threads, seconds, 0)
+    f1, t1 = sample(1, seconds / 3.0, frames)
+    return {"value": frames * k_info / t_all, "unit": "info-bits/s", "cores": threads, "kind": "port",
+            "value_1thread": f1 * k_info / t1 if t1 > 0 else None,
+            "host": cpus,
+            "sample": f"{frames} frames of the same workload (chunks of {threads * 4}), {t_all:.1f} s, "
+                      f"oracle/ldpc_oracle.c on {threads} host threads (all CPUs this job may use: nproc "
+                      f"{cpus['nproc']}, affinity {cpus['affinity']}, cgroup quota {cpus['cgroup_quota']}; "
+                      f"{cpus['model']}); 1 thread: {f1} frames in {t1:.1f} s"}
 
 
 if __name__ == "__main__":

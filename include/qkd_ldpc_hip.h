@@ -91,6 +91,19 @@ int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr,
                                const int32_t *col_idx, const int32_t *col_ptr,
                                const int32_t *row_idx, int32_t device_mask, qldpc_graph **out);
 
+/* As qldpc_graph_create, on an explicit list of HIP devices, one shard per
+ * entry: qldpc_decode_batch splits a batch in ndevices contiguous slices, one
+ * host thread, stream and graph replica per entry.  A device may be listed
+ * more than once (several concurrent shards on one GPU). */
+int qldpc_graph_create_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                          const int32_t *devices, int32_t ndevices, qldpc_graph **out);
+
+/* Plan only, on the host (no device is touched): the returned graph has no
+ * devices and cannot decode; it answers qldpc_graph_info and
+ * qldpc_graph_labels.  For inspection and CPU tests of the planner. */
+int qldpc_graph_create_host(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                            qldpc_graph **out);
+
 void qldpc_graph_destroy(qldpc_graph *g);
 
 /* n, m, nnz and the number of devices the graph lives on. */
@@ -157,6 +170,21 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
 int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, int32_t *lanes,
                      int32_t *edges_per_lane, int32_t *workgroups, int32_t *lds_bytes,
                      const char **variant);
+
+/* The decoder's bank-aware label of every bit id (labels_out: n entries; the
+ * identity when the plan keeps the reference's ids — split, hybrid and
+ * first-generation shapes), and stats_out (nullable, 4 entries): summed LDS
+ * bank excess of the slot layout before / after the relabelling search, and
+ * the summed busiest-bank counts (LDS cycles of the slot groups) before / after.  Labels never change results: inputs and outputs
+ * of every entry point use the reference's bit ids. */
+int qldpc_graph_labels(const qldpc_graph *g, int32_t *labels_out, int64_t *stats_out);
+
+/* Kernel timing: while enabled on g, every decode kernel launch is bracketed
+ * by HIP events on the stream it runs on (nothing else: not the frame build,
+ * the claim order or the key compare).  qldpc_last_decode_kernel_ms waits for
+ * the last timed launch on (device, stream) and returns its duration in ms. */
+int qldpc_set_kernel_timing(qldpc_graph *g, int32_t enabled);
+int qldpc_last_decode_kernel_ms(qldpc_graph *g, int32_t device, void *stream, float *ms);
 
 /* Diagnostic: evaluate the decoder's device math on `count` inputs on the
  * current device — fn 0 tanh, 1 atanh, 2 expm1, 3 log1p (exact_math.h, the

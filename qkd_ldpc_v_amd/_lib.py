@@ -19,6 +19,8 @@ if os.environ.get("QLDPC_DIAG_STAMPS") == "1":  # diagnostic phase-stamp build (
     LIB_PATH = os.path.join(_HERE, "diag", "libqkdldpc_hip.so")
 if os.environ.get("QLDPC_AB_BUILD"):  # A/B experiments: an alternative in-tree build, qkd_ldpc_v_amd/ab/<name>/
     LIB_PATH = os.path.join(_HERE, "ab", os.environ["QLDPC_AB_BUILD"], "libqkdldpc_hip.so")
+if os.environ.get("QLDPC_ASAN") == "1":  # `make asan`: host code under ASan + UBSan (build/asan/)
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "asan", "libqkdldpc_hip.so")
 
 QLDPC_OK = 0
 ERROR_NAMES = {-1: "EINVAL", -2: "EHIP", -3: "EIO", -4: "ENOMEM", -5: "EUNSUP"}
@@ -57,7 +59,12 @@ _SIGNATURES = {
     "qldpc_load_matrix": (_I32, [ctypes.c_char_p, _I32, _PI32, _PI32, _PI32, _P, _P, _P, _P, _PI32]),
     "qldpc_graph_create": (_I32, [_I32, _I32, _P, _P, _I32, ctypes.POINTER(_P)]),
     "qldpc_graph_create_checked": (_I32, [_I32, _I32, _P, _P, _P, _P, _I32, ctypes.POINTER(_P)]),
+    "qldpc_graph_create_on": (_I32, [_I32, _I32, _P, _P, _P, _I32, ctypes.POINTER(_P)]),
+    "qldpc_graph_create_host": (_I32, [_I32, _I32, _P, _P, ctypes.POINTER(_P)]),
+    "qldpc_graph_labels": (_I32, [_P, _P, _P]),
     "qldpc_graph_destroy": (None, [_P]),
+    "qldpc_set_kernel_timing": (_I32, [_P, _I32]),
+    "qldpc_last_decode_kernel_ms": (_I32, [_P, _I32, _P, ctypes.POINTER(ctypes.c_float)]),
     "qldpc_graph_info": (_I32, [_P, _PI32, _PI32, _PI32, _PI32]),
     "qldpc_graph_plan": (_I32, [_P, _I32, _I32, _PI32, _PI32, _PI32, _PI32, ctypes.POINTER(ctypes.c_char_p)]),
     "qldpc_decode_batch": (_I32, [_P, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P, _P, _P, _P]),
@@ -103,7 +110,11 @@ def lib() -> ctypes.CDLL:
             )
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None and os.environ.get("QLDPC_AB_BUILD"):
+                continue  # an older A/B build may predate an entry point
+            if fn is None:
+                raise ImportError(f"{LIB_PATH} does not export {name}: rebuild it (make)")
             fn.restype = res
             fn.argtypes = args
         _lib = L

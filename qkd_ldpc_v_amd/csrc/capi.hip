@@ -27,6 +27,7 @@
 #include "../../include/qkd_ldpc_hip.h"
 #include "decoder.hpp"
 #include "loaders.hpp"
+#include "relabel.hpp"
 
 using namespace qldpc;
 
@@ -66,6 +67,9 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     // frame claim order (order.hip): per-frame weights and the sorted order
     int32_t *fweight = nullptr, *forder = nullptr;
     size_t order_frames = 0;
+    // kernel timing (qldpc_set_kernel_timing): events around the last decode launch
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool ev_recorded = false;
 };
 
 struct HostIO {  // device staging buffers of the host-buffer entry
@@ -95,6 +99,8 @@ struct DeviceGraph {
     uint32_t *vng_rec = nullptr;  // register-shape bit gather: per slot, the code word's byte offset | shift << 16
     uint64_t *row_sem = nullptr;    // V2 scan: [wave][slot][4] START / END / PARK lane masks (+ pad)
     uint64_t *row_rmask = nullptr;  // V2 scan: [row j][lane] slots of the lane's j-th started row
+    int32_t *col_orig = nullptr, *col_lab = nullptr;  // V2 bank relabelling: label -> bit id, bit id -> label
+    int32_t *ell_lab = nullptr;     // row-ELL in labels (the claim order reads label-ordered frame codes)
     std::mutex mu;     // workspaces (ws), occupancy cache
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
@@ -163,6 +169,9 @@ struct qldpc_graph {
     int nst_max = 0;                        // V2 SPA scan: most rows started in one lane (row_rmask rows)
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
+    bool kernel_timing = false;             // qldpc_set_kernel_timing
+    std::vector<int32_t> col_lab;           // V2 bank relabelling (relabel.cpp): bit id -> label; empty: identity
+    long long relabel_stats[4] = {0, 0, 0, 0};  // bank excess before / after, busiest-bank cycles before / after
     std::vector<int> part_row0;             // V2 split: first layout row of each part (+ m)
     std::vector<std::unique_ptr<DeviceGraph>> devs;
 };
@@ -309,6 +318,9 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
     const long long E = g.E;
     const int forced = env_int("QLDPC_V2_WAVES", 0);
     const int shapes[4][2] = {{V2_R_TIGHT, 0}, {V2_R_SMALL, 0}, {V2_R_MID, 0}, {V2_R_SMALL, V2_RG_HYBRID}};
+    // register shapes (RG == 0) scan from 64-bit lane-mask rows of at most 63
+    // slots (row_rmask bit 63 marks a row continuing into the next lane)
+    static_assert(V2_R_TIGHT <= 63 && V2_R_SMALL <= 63 && V2_R_MID <= 63, "register shape beyond the scan's masks");
     for (const auto &sh : shapes) {
         const int R = sh[0] + sh[1];  // slots per lane
         const int wmax = v2_threads_for(sh[0]) / 64;
@@ -447,8 +459,21 @@ int upload(T **dst, const std::vector<T> &src) {
     return QLDPC_OK;
 }
 
+// Labellings already searched in this process (relabel.cpp takes ~0.5 s on a
+// 10k code; tests and drivers create graphs of one H many times).  Keyed by a
+// hash of everything the search reads, verified by a full compare on a hit.
+struct RelabelMemo {
+    std::vector<int32_t> key;  // n, m, waves, mode, iters, row_ptr..., col_idx...
+    std::vector<int32_t> lab;
+    long long stats[4];
+};
+std::mutex g_relabel_mu;
+std::vector<RelabelMemo> g_relabel_memo;  // most recent last, at most 8
+
+// host_only: plan and relabel without any device (introspection; the graph
+// has no devices and cannot decode).
 int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx, int32_t device_mask,
-                qldpc_graph **out) {
+                qldpc_graph **out, bool host_only = false, const std::vector<int> *device_list = nullptr) {
     if (!out) return fail(QLDPC_EINVAL, "out is NULL");
     *out = nullptr;
     if (n <= 0 || m < 0 || !row_ptr || (!col_idx && row_ptr[m] > 0))
@@ -540,6 +565,75 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             }
         }
     }
+    // Bank-aware relabelling of bit ids (relabel.cpp), one-workgroup register
+    // shapes: the (wave, slot, half) groups of both slot layouts (CSR order for
+    // the SPA family, kpos order for min-sum) read total[label] with distinct
+    // banks, and the min-sum bit gather's code-word ORs (dv <= 4) hit distinct
+    // banks too.  The metadata, vn_rows and vng_rec then carry labels; the frame
+    // codes are written in label order and the decoder maps its outputs back.
+    // QLDPC_RELABEL=0: identity (A/B).
+    std::vector<int32_t> col_r;
+    const int32_t *colL = col_idx;  // the metadata's bit ids
+    const int relabel_mode = env_int("QLDPC_RELABEL", 1);  // (A/B: 2 CSR layout only, 3 kpos layout only)
+    if (v2 && g->split_k <= 1 && g->v2RG == 0 && relabel_mode != 0) {
+        const bool word = v2_vng_ok(2, g->v2R, g->v2RG, g->split_k, g->dv_max, m);
+        std::vector<RelabelGroup> groups;
+        for (int sorted = 0; sorted < 2; ++sorted) {
+            if ((relabel_mode == 2 && sorted) || (relabel_mode == 3 && !sorted)) continue;
+            std::vector<int> pm(ledge);
+            if (sorted)
+                for (int j = 0; j < m; ++j)
+                    std::stable_sort(pm.begin() + lrp[j], pm.begin() + lrp[j + 1],
+                                     [&](int x, int y) { return kpos[x] < kpos[y]; });
+            for (int w = 0; w < T / 64; ++w) {
+                const long long wb = lrp[g->wave_rows[w]], we = lrp[g->wave_rows[w + 1]];
+                const int epl_w = std::max<int>((int)((we - wb + 63) / 64), g->max_dc);
+                if (we == wb) continue;
+                for (int k = 0; k < epl_w; ++k)
+                    for (int h = 0; h < 2; ++h) {
+                        RelabelGroup grp;
+                        for (int li = 32 * h; li < 32 * h + 32; ++li) {
+                            const long long e = wb + (long long)li * epl_w + k;
+                            if (e < we) {
+                                const int ed = pm[e];
+                                grp.members.push_back({col_idx[ed], 0, (uint8_t)(1 | ((sorted && word && kpos[ed] < 4) ? 2 : 0))});
+                            } else {
+                                grp.members.push_back({-1, n % 128, 1});  // dummy slot: column n
+                            }
+                        }
+                        groups.push_back(std::move(grp));
+                    }
+            }
+        }
+        const int iters = env_int("QLDPC_RELABEL_ITERS", 16);  // search moves per edge
+        std::vector<int32_t> key = {n, m, T / 64, relabel_mode, iters};
+        key.insert(key.end(), row_ptr, row_ptr + m + 1);
+        key.insert(key.end(), col_idx, col_idx + E);
+        {
+            std::lock_guard<std::mutex> lk(g_relabel_mu);
+            for (const auto &me : g_relabel_memo)
+                if (me.key == key) {
+                    g->col_lab = me.lab;
+                    std::copy(me.stats, me.stats + 4, g->relabel_stats);
+                    break;
+                }
+        }
+        if (g->col_lab.empty()) {
+            RelabelStats st;
+            g->col_lab = bank_relabel(n, groups, 0x5eed0ba4c5ull, (long long)iters * E, &st);
+            g->relabel_stats[0] = st.excess_before;
+            g->relabel_stats[1] = st.excess_after;
+            g->relabel_stats[2] = st.cycles_before;
+            g->relabel_stats[3] = st.cycles_after;
+            std::lock_guard<std::mutex> lk(g_relabel_mu);
+            if (g_relabel_memo.size() >= 8) g_relabel_memo.erase(g_relabel_memo.begin());
+            g_relabel_memo.push_back({std::move(key), g->col_lab, {g->relabel_stats[0], g->relabel_stats[1],
+                                                                    g->relabel_stats[2], g->relabel_stats[3]}});
+        }
+        col_r.resize(E);
+        for (int e = 0; e < E; ++e) col_r[e] = g->col_lab[col_idx[e]];
+        colL = col_r.data();
+    }
     // Hybrid shape: VN terms kk >= vn_k0 go through a per-frame stage, laid out
     // term-major over the bits of degree > kk, bits ordered by degree
     // (descending) so each term's bits are a prefix: stage[off[kk] + rank[b]].
@@ -585,7 +679,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             vn_rows.assign((size_t)2 * n, 0xFFFFFFFFu);
             for (int r = 0; r < m; ++r)
                 for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
-                    uint32_t &w = vn_rows[(size_t)2 * col_idx[e] + (kpos[e] >> 1)];
+                    uint32_t &w = vn_rows[(size_t)2 * colL[e] + (kpos[e] >> 1)];
                     const int sh = 16 * (kpos[e] & 1);
                     w = (w & ~(0xFFFFu << sh)) | ((uint32_t)lrow_of[r] << sh);
                 }
@@ -668,14 +762,14 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                     } else {
                         const int j = lrow[e];
                         const int ed = perm[e];  // the edge at that position
-                        wd = (uint32_t)col_idx[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
+                        wd = (uint32_t)colL[ed] | ((uint32_t)kpos[ed] << META_KPOS_SHIFT) | META_VALID;
                         if (v2) {
                             vnm[(size_t)w * g->dv_max + kpos[ed]] |= 1ull << k;
                             vex[((size_t)w * g->dv_max + kpos[ed]) * S4 + k] |= 1ull << li;
                         }
                         if (sorted && vng_h) vng_meta2[midx(l, k)] = (uint32_t)(P0[col_idx[ed]] + kpos[ed]);
                         if (sorted && !vng_rec.empty() && kpos[ed] < 4) {
-                            const uint32_t c = (uint32_t)col_idx[ed];
+                            const uint32_t c = (uint32_t)colL[ed];
                             vng_rec[midx(l, k)] = (c & ~3u) | ((((c & 3u) << 3) + 2u * (uint32_t)kpos[ed]) << 16);
                         }
                         if (g->n_hd && kpos[ed] >= g->vn_k0)
@@ -740,6 +834,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         "\"dv_max\": %d, \"vn_slot_visits_csr\": %lld, \"vn_slot_visits_kpos_sorted\": %lld, "
                         "\"vn_slot_visits_unmasked\": %lld}}\n",
                 W, g->v2R, g->v2RG, g->EPL, g->dv_max, visited(vnm), visited(vnm_ms), full);
+        fprintf(stderr, "{\"relabel\": {\"excess_before\": %lld, \"excess_after\": %lld, \"cycles_before\": %lld, "
+                        "\"cycles_after\": %lld}}\n",
+                g->relabel_stats[0], g->relabel_stats[1], g->relabel_stats[2], g->relabel_stats[3]);
     }
     // Row-ELL (slot-major) for syndrome evaluation.
     const int dcm = std::max(1, g->max_dc);
@@ -749,10 +846,27 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         for (int k = 0; k < rdeg[j]; ++k) ell[(size_t)k * m + j] = col_idx[row_ptr[j] + k];
     }
 
+    std::vector<int32_t> ell_lab, col_orig;
+    if (!g->col_lab.empty()) {
+        ell_lab = ell;
+        for (int j = 0; j < m; ++j)
+            for (int k = 0; k < rdeg[j]; ++k) ell_lab[(size_t)k * m + j] = g->col_lab[ell[(size_t)k * m + j]];
+        col_orig.resize(n);
+        for (int i = 0; i < n; ++i) col_orig[g->col_lab[i]] = i;
+    }
+    if (host_only) {
+        *out = g.release();
+        return QLDPC_OK;
+    }
+
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     std::vector<int> devices;
-    if (device_mask == 0) {
+    if (device_list) {
+        for (int d : *device_list)
+            if (d < 0 || d >= ndev) return fail(QLDPC_EINVAL, "device list names a device that does not exist");
+        devices = *device_list;
+    } else if (device_mask == 0) {
         int cur = 0;
         HIP_TRY(hipGetDevice(&cur));
         devices.push_back(cur);
@@ -785,7 +899,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->vn_rows, vn_rows)) || (rc = upload(&dg->vng_bits, vng_bits)) ||
             (rc = upload(&dg->vng_meta2, vng_meta2)) || (rc = upload(&dg->row_sem, row_sem)) ||
             (rc = upload(&dg->vng_rec, vng_rec)) ||
-            (rc = upload(&dg->row_rmask, row_rmask))) {
+            (rc = upload(&dg->row_rmask, row_rmask)) ||
+            (!col_orig.empty() && ((rc = upload(&dg->col_orig, col_orig)) || (rc = upload(&dg->col_lab, g->col_lab)) ||
+                                   (rc = upload(&dg->ell_lab, ell_lab))))) {
             (void)hipSetDevice(prev);
             return rc;
         }
@@ -957,6 +1073,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
     a.row_orig = dg->row_orig;
+    a.col_orig = dg->col_orig;
+    a.col_lab = dg->col_lab;
     a.row_sem = (v2 && g->nst_max > 0) ? dg->row_sem : nullptr;
     a.row_rmask = (v2 && g->nst_max > 0) ? dg->row_rmask : nullptr;
     a.nst_max = g->nst_max;
@@ -995,14 +1113,19 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
             return fail(QLDPC_EUNSUP, "this code's min-sum row aggregates need the bit gather (QLDPC_VNG=0 given)");
     }
     if (v2 && !codes_ready)
-        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, stream));
-    {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order)
+        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, dg->col_orig, stream));
+    {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order).
+        // It only schedules — results never depend on it — so a shape it cannot
+        // run (LDS beyond the device limit) decodes in index order instead.
         const char *e = std::getenv("QLDPC_ORDER");
         if (!(e && std::strcmp(e, "0") == 0) && batch > 1) {
-            HIP_TRY(launch_frame_order(g->n, g->m, dg->ell_col, dg->row_deg, batch, synd, llr,
-                                       v2 ? w->codes : nullptr, w->palette, w->pal_ok, w->fweight, w->forder,
-                                       stream));
-            a.frame_order = w->forder;
+            // (relabelled graphs: the frame codes are in label order, so is the row-ELL it reads)
+            const hipError_t oe = launch_frame_order(g->n, g->m, dg->col_orig ? dg->ell_lab : dg->ell_col,
+                                                     dg->row_deg, batch, synd, llr, v2 ? w->codes : nullptr,
+                                                     w->palette, w->pal_ok, w->fweight, w->forder, dg->col_orig,
+                                                     stream);
+            if (oe == hipSuccess) a.frame_order = w->forder;
+            else (void)hipGetLastError();  // clear the sticky launch error; index order
         }
     }
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
@@ -1013,8 +1136,17 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
     a.stamps = d_st;
 #endif
+    if (g->kernel_timing) {  // (the workspace is per stream: no other call records on these events)
+        if (!w->ev0) HIP_TRY(hipEventCreate(&w->ev0));
+        if (!w->ev1) HIP_TRY(hipEventCreate(&w->ev1));
+        HIP_TRY(hipEventRecord(w->ev0, stream));
+    }
     if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
     else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
+    if (g->kernel_timing) {
+        HIP_TRY(hipEventRecord(w->ev1, stream));
+        w->ev_recorded = true;
+    }
 #ifdef QL_PHASE_STAMPS
     {  // diagnostic: per-phase share of wave time, one JSON line on stderr
         std::vector<uint64_t> h(nst);
@@ -1117,6 +1249,27 @@ int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr, con
     return build_graph(n, m, row_ptr, col_idx, device_mask, out);
 }
 
+int qldpc_graph_create_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                          const int32_t *devices, int32_t ndevices, qldpc_graph **out) {
+    if (!devices || ndevices <= 0 || ndevices > 64) return fail(QLDPC_EINVAL, "need 1..64 devices");
+    const std::vector<int> list(devices, devices + ndevices);
+    return build_graph(n, m, row_ptr, col_idx, 0, out, false, &list);
+}
+
+int qldpc_graph_create_host(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                            qldpc_graph **out) {
+    return build_graph(n, m, row_ptr, col_idx, 0, out, true);
+}
+
+int qldpc_graph_labels(const qldpc_graph *g, int32_t *labels_out, int64_t *stats_out) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    if (labels_out)
+        for (int i = 0; i < g->n; ++i) labels_out[i] = g->col_lab.empty() ? i : g->col_lab[i];
+    if (stats_out)
+        for (int i = 0; i < 4; ++i) stats_out[i] = g->relabel_stats[i];
+    return QLDPC_OK;
+}
+
 void qldpc_graph_destroy(qldpc_graph *g) {
     if (!g) return;
     int prev = 0;
@@ -1150,6 +1303,9 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->vng_rec);
         (void)hipFree(d->row_sem);
         (void)hipFree(d->row_rmask);
+        (void)hipFree(d->col_orig);
+        (void)hipFree(d->col_lab);
+        (void)hipFree(d->ell_lab);
         for (auto &kv : d->ws) {
             (void)hipFree(kv.second.counter);
             (void)hipFree(kv.second.scratch);
@@ -1157,6 +1313,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(kv.second.palette);
             (void)hipFree(kv.second.pal_ok);
             (void)hipFree(kv.second.split_ctl);
+            if (kv.second.ev0) (void)hipEventDestroy(kv.second.ev0);
+            if (kv.second.ev1) (void)hipEventDestroy(kv.second.ev1);
             (void)hipFree(kv.second.gtotal);
             (void)hipFree(kv.second.gstage);
         }
@@ -1201,6 +1359,35 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
         if (e != hipSuccess) return hip_fail(e, "occupancy");
         *workgroups = b * dg->num_cus;
     }
+    return QLDPC_OK;
+}
+
+int qldpc_set_kernel_timing(qldpc_graph *g, int32_t enabled) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    g->kernel_timing = enabled != 0;
+    return QLDPC_OK;
+}
+
+int qldpc_last_decode_kernel_ms(qldpc_graph *g, int32_t device, void *stream, float *ms) {
+    if (!g || !ms) return fail(QLDPC_EINVAL, "graph / ms is NULL");
+    DeviceGraph *dg = find_dev(g, device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(dg->mu);
+        auto it = dg->ws.find(stream);
+        if (it == dg->ws.end() || !it->second.ev_recorded)
+            return fail(QLDPC_EINVAL, "no timed decode launch on that stream (qldpc_set_kernel_timing)");
+        e0 = it->second.ev0;
+        e1 = it->second.ev1;
+    }
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    hipError_t e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return hip_fail(e, "decode kernel events");
     return QLDPC_OK;
 }
 
@@ -1308,7 +1495,8 @@ int qldpc_build_frames_device(qldpc_graph *g, int32_t device, int32_t batch, con
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
     hipError_t e = launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob,
-                                       d_log_p, d_llr, d_syndrome, nullptr, nullptr, nullptr, (hipStream_t)stream);
+                                       d_log_p, d_llr, d_syndrome, nullptr, nullptr, nullptr, nullptr,
+                                       (hipStream_t)stream);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return hip_fail(e, "build_frames");
     return QLDPC_OK;
@@ -1362,7 +1550,7 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
             codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
         }
         HIP_TRY(launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob, d_log_p,
-                                    d_llr_ws, d_synd_ws, codes, palette, pal_ok, s));
+                                    d_llr_ws, d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
         int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
                           g->variant == VAR_V2);
         if (r) return r;
@@ -1525,7 +1713,7 @@ int qldpc_build_frames_rate_adapt_device(qldpc_graph *g, const qldpc_rate_plan *
     HIP_TRY(hipSetDevice(device));
     hipError_t e = launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
                                           d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, d_llr,
-                                          d_syndrome, nullptr, nullptr, nullptr, (hipStream_t)stream);
+                                          d_syndrome, nullptr, nullptr, nullptr, nullptr, (hipStream_t)stream);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return hip_fail(e, "build_frames_rate_adapt");
     return QLDPC_OK;
@@ -1567,7 +1755,7 @@ int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan
         }
         HIP_TRY(launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
                                        d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, d_llr_ws,
-                                       d_synd_ws, codes, palette, pal_ok, s));
+                                       d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
         int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
                           g->variant == VAR_V2);
         if (r) return r;

@@ -308,7 +308,8 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
                                                            const int32_t *row_deg, const uint8_t *alice,
                                                            const uint8_t *bob, const double *log_p,
                                                            double *llr, uint8_t *synd, uint8_t *codes,
-                                                           double *palette, uint8_t *pal_ok) {
+                                                           double *palette, uint8_t *pal_ok,
+                                                           const int32_t *col_orig) {
     const size_t f = blockIdx.x;
     const double lp = log_p[f];
     const uint8_t *al = alice + f * (size_t)n;
@@ -317,13 +318,15 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
         double *l = llr + f * (size_t)n;
         for (int i = threadIdx.x; i < n; i += blockDim.x) l[i] = bo[i] ? -lp : lp;
     }
-    if (codes) {  // V2 palette form: code 0 = +log_p, 1 = -log_p
+    if (codes) {  // V2 palette form: code 0 = +log_p, 1 = -log_p; in label order (col_orig)
         const int nc = (n + 3) / 4;
         uint8_t *cs = codes + f * (size_t)nc;
         for (int j = threadIdx.x; j < nc; j += blockDim.x) {
             int byte = 0;
-            for (int s = 0; s < 4; ++s)
-                if (4 * j + s < n && bo[4 * j + s]) byte |= 1 << (2 * s);
+            for (int s = 0; s < 4; ++s) {
+                const int i = 4 * j + s;
+                if (i < n && bo[col_orig ? col_orig[i] : i]) byte |= 1 << (2 * s);
+            }
             cs[j] = (uint8_t)byte;
         }
         if (threadIdx.x < 4) palette[f * 4 + threadIdx.x] = threadIdx.x == 1 ? -lp : lp;  // unused 2, 3 repeat entry 0
@@ -349,8 +352,11 @@ __global__ void __launch_bounds__(256) keys_match_kernel(int n, const uint8_t *a
 }
 
 __global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, const double *in, double *out) {
-    __shared__ ql_exact::Expm1Class ctab[ql_exact::EXPM1_CLASSES];  // fn 8: the SPA scan's table form
-    if (threadIdx.x < ql_exact::EXPM1_CLASSES) ctab[threadIdx.x] = ql_exact::expm1_class(threadIdx.x + ql_exact::EXPM1_K_MIN);
+    __shared__ ql_exact::Expm1A ctab_a[ql_exact::EXPM1_CLASSES];  // fn 8: the SPA scan's table form
+    __shared__ ql_exact::Expm1B ctab_b[ql_exact::EXPM1_CLASSES];
+    if (threadIdx.x < ql_exact::EXPM1_CLASSES)
+        ql_exact::expm1_class(threadIdx.x + ql_exact::EXPM1_K_MIN, &ctab_a[threadIdx.x], &ctab_b[threadIdx.x]);
+    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b};
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -431,11 +437,11 @@ hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_
 hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
                                int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
-                               hipStream_t stream) {
+                               const int32_t *col_orig, hipStream_t stream) {
     (void)max_dc;
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, alice,
-                       bob, log_p, llr, synd, codes, palette, pal_ok);
+                       bob, log_p, llr, synd, codes, palette, pal_ok, col_orig);
     return hipGetLastError();
 }
 

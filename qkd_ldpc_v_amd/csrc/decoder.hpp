@@ -135,6 +135,11 @@ struct DecodeArgs {
     // (C5 R=0.5: m = 5120): rowAB lives in the workgroup's global scratch
     // (L2-resident) at this offset in doubles; -1: rows in LDS.
     long long rows_wg_offset;
+    // Bank-aware bit labels (relabel.cpp; one-workgroup register shapes): the
+    // graph's metadata and the frame codes use labels, llr / bits / posterior
+    // the reference's bit ids.  nullptr: identity.
+    const int32_t *col_orig;        // [n] label -> bit id
+    const int32_t *col_lab;         // [n] bit id -> label
 };
 
 // The persistent decoders' frame claim: the next frame of the launch's claim
@@ -157,7 +162,7 @@ hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_
 hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
                                int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
-                               hipStream_t stream);
+                               const int32_t *col_orig, hipStream_t stream);
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0,
@@ -170,7 +175,7 @@ constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per la
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, hipStream_t stream);
+                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
 size_t trials_lds_bytes(int n);
 size_t trials_scratch_words(int n, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
@@ -180,14 +185,14 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
                                   const int32_t *src, int n_punct, int batch, const uint8_t *alice, const uint8_t *bob,
                                   const uint8_t *palice, const uint8_t *pbob, const double *log_p, uint8_t *alice_ext,
                                   double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
-                                  hipStream_t stream);
+                                  const int32_t *col_orig, hipStream_t stream);
 // Claim order of a batch: frames by ascending weight of the channel decision's
 // syndrome mismatch (order.hip).  llr is read only for frames without codes.
 size_t frame_weight_lds(int n);
 hipError_t launch_frame_order(int n, int m, const int32_t *ell_col, const int32_t *row_deg, int batch,
                               const uint8_t *synd, const double *llr, const uint8_t *codes,
                               const double *palette, const uint8_t *pal_ok, int32_t *weight, int32_t *order,
-                              hipStream_t stream);
+                              const int32_t *col_orig, hipStream_t stream);
 hipError_t launch_math_selftest(int fn, int count, const double *in, double *out, hipStream_t stream);
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits,
                              uint8_t *match, hipStream_t stream);

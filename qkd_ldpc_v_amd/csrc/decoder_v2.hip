@@ -68,7 +68,7 @@ struct V2Layout {
         tail = o;     // (min-sum: a lane's tail aggregate is parked in its row's rowAB entry)
         tailneg = o;
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
-        ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * sizeof(ql_exact::Expm1Class)));  // SPA: tanh's expm1 classes
+        ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * (sizeof(ql_exact::Expm1A) + sizeof(ql_exact::Expm1B))));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         // one workgroup per frame: the rows' target syndrome bits as sign words
         // (s << 31), in the palette-index area past the codes when it has room
@@ -237,10 +237,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     if (tid == 0) *s_flag = 0;
     // SPA: the expm1 class table of tanh_half_clip_t, once per workgroup (the
     // frame loop's first barrier orders it before any scan)
-    const ql_exact::Expm1Class *const ctab = reinterpret_cast<const ql_exact::Expm1Class *>(smem + L.ctab);
+    // (two arrays of 16-byte entries: A at L.ctab, B right after A)
+    ql_exact::Expm1A *const ctab_a = reinterpret_cast<ql_exact::Expm1A *>(smem + L.ctab);
+    ql_exact::Expm1B *const ctab_b = reinterpret_cast<ql_exact::Expm1B *>(smem + L.ctab) + ql_exact::EXPM1_CLASSES;
+    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b};
     if constexpr (ALG == 0) {
         if (tid < ql_exact::EXPM1_CLASSES)
-            reinterpret_cast<ql_exact::Expm1Class *>(smem + L.ctab)[tid] = ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN);
+            ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN, &ctab_a[tid], &ctab_b[tid]);
     }
 #ifdef QL_PHASE_STAMPS
     uint64_t st_acc[NUM_STAMPS];
@@ -381,7 +384,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 if (paletted) return pal[codes[col]];
             }
-            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
+            // (llr[] is in the reference's bit order: map a label back)
+            const int cg = a.col_orig ? a.col_orig[col] : col;
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, cg * 8, 0, 0));
         };
         // total starts as the channel LLRs: the check-node scan of iteration 0
         // reads the channel decision from it, and bits of degree 0 keep it.
@@ -617,7 +622,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     if (b < n) {
                         rr = ld_rows(b);
                         if (paletted) gcn = __builtin_amdgcn_raw_buffer_load_b8(gc_rs, b >> 2, 0, 0);
-                        else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, b * 8, 0, 0));
+                        else lrn = llr_of(b);
                     }
                     for (; b < n; b += T) {
                         const uint2 cur = rr;
@@ -627,7 +632,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         if (bn < n) {
                             rr = ld_rows(bn);
                             if (paletted) gcn = __builtin_amdgcn_raw_buffer_load_b8(gc_rs, bn >> 2, 0, 0);
-                            else lrn = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, bn * 8, 0, 0));
+                            else lrn = llr_of(bn);
                         }
                         const uint32_t cb = codes[b];
                         codes[b] = 0;
@@ -1102,8 +1107,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const bool zero_post = ADAPT && !had_vn;
         uint8_t *bits = a.bits + (size_t)f * n;
         double *post = a.post ? a.post + (size_t)f * n : nullptr;
+        // (relabelled graphs: bit i's total sits at its label)
+        const int32_t *const clab = a.col_lab;
         for (int i = bit_lo + tid; i < bit_hi; i += T) {
-            const double z = total[i];
+            const double z = total[clab ? clab[i] : i];
             bits[i] = (z <= 0.0) ? 1 : 0;
             if (post) post[i] = zero_post ? 0.0 : z;
         }
@@ -1129,7 +1136,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 // with more gets pal_ok = 0 and the decoder gathers its llr[] instead.  Unused
 // entries repeat entry 0 (the SPA iteration-0 test reads all four).
 __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const double *llr, uint8_t *codes,
-                                                        double *palette, uint8_t *pal_ok) {
+                                                        double *palette, uint8_t *pal_ok, const int32_t *col_orig) {
     __shared__ unsigned long long pv[4];
     __shared__ int pcount, over;
     const size_t f = blockIdx.x;
@@ -1167,11 +1174,13 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
     for (int j = threadIdx.x; j < nc; j += blockDim.x) {
         int byte = 0;
         for (int s = 0; s < 4; ++s) {
-            const int i = 4 * j + s;
+            const int i = 4 * j + s;  // a label (col_orig: the codes are in label order)
             int code = 0;
-            if (i < n)
+            if (i < n) {
+                const unsigned long long x = v[col_orig ? col_orig[i] : i];
                 for (int q = 1; q < 4; ++q)
-                    if (q < cnt && v[i] == pv[q]) code = q;
+                    if (q < cnt && x == pv[q]) code = q;
+            }
             byte |= code << (2 * s);
         }
         cs[j] = (uint8_t)byte;
@@ -1247,6 +1256,7 @@ bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
 
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
     // the scan of one-workgroup register frames reads the row structure masks
+    // (plan_v2 only builds register shapes of <= 63 slots, which always get row_sem)
     if (a.split_k <= 1 && a.v2RG == 0 && !a.row_sem) return hipErrorInvalidValue;
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
@@ -1270,9 +1280,10 @@ hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_b
 }
 
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, hipStream_t stream) {
+                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    hipLaunchKernelGGL(palettize_kernel, dim3(batch), dim3(256), 0, stream, n, nc, llr, codes, palette, pal_ok);
+    hipLaunchKernelGGL(palettize_kernel, dim3(batch), dim3(256), 0, stream, n, nc, llr, codes, palette, pal_ok,
+                       col_orig);
     return hipGetLastError();
 }
 

@@ -666,28 +666,28 @@ QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
 // Table form of the per-class constants above.  They depend on k alone, and
 // the common path only reaches k in [-3, 63] (u in (-2, 0] or [2, 44)), so a
 // 67-entry table indexed by k + 3 holds X3, X4 and B and the exponent addend
-// k << 20, and also s_tanh.c's tail constants: |x| >= 1 exactly when k > 0
-// (u >= 2 gives k >= 3, u in (-2, 0] gives k in [-3, 0]), so C and the
-// numerator -2 / -y are class constants too: num = fma(y, NM, NA) with
-// (NM, NA) = (0, -2) or (-1, -0) — y * 0 + -2 == -2 and y * -1 + -0 == -y
-// exactly for finite y (signed zeros included).  The constants are stored as
-// whole doubles (four 16-byte LDS reads land them in register pairs: no
-// assembly of hi words over a zero low word).  Same constants, same IEEE
-// operations as tanh_half_common.
-#ifndef QL_CTAB
-#define QL_CTAB 32  // entry bytes: 32 (B and C as high words: fewer live registers) or 64 (all doubles)
-#endif
-struct alignas(16) Expm1Class {
-#if QL_CTAB == 64
-    double x3, x4, b, c, nm, na;
-    uint32_t k20, pad[3];
-#else
+// k << 20, and also s_tanh.c's tail constant C: |x| >= 1 exactly when k > 0
+// (u >= 2 gives k >= 3, u in (-2, 0] gives k in [-3, 0]).  X3 and X4 are whole
+// doubles (a 16-byte LDS read lands them in register pairs: no assembly of hi
+// words over a zero low word); B and C as high words.  Same constants, same
+// IEEE operations as tanh_half_common.
+// The table is two arrays of 16-byte entries (A: X3, X4; B: B, C, k << 20),
+// not one of 32-byte entries: a wave's lanes read entries of different k
+// together, and at a 16-byte stride the k's of a 16-lane ds_read_b128 group
+// spread over all 16 bank slots of the 256-byte bank row instead of every
+// other one (half the bank conflicts; MI355X_MICROARCH.md §LDS).
+struct alignas(16) Expm1A {
     double x3, x4;
+};
+struct alignas(16) Expm1B {
     uint32_t b_hi, c_hi, k20, pad;
-#endif
+};
+struct Expm1Tab {
+    const Expm1A *a;
+    const Expm1B *b;
 };
 constexpr int EXPM1_K_MIN = -3, EXPM1_K_MAX = 63, EXPM1_CLASSES = EXPM1_K_MAX - EXPM1_K_MIN + 1;
-QL_HD Expm1Class expm1_class(int32_t k) {
+QL_HD void expm1_class(int32_t k, Expm1A *ea, Expm1B *eb) {
     const uint32_t ku = (uint32_t)k;
     const bool fcls = (ku - 20u) <= 36u;
     const bool far = (ku + 1u) > 57u;
@@ -695,34 +695,23 @@ QL_HD Expm1Class expm1_class(int32_t k) {
     uint32_t a_hi = 0x3ff00000u - (0x200000u >> (ku & 31u));
     a_hi = (k == 0) ? 0x80000000u : a_hi;
     a_hi = (k == -1) ? 0xbff00000u : a_hi;
-    Expm1Class c;
-    c.x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
-    c.x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
-#if QL_CTAB == 64
-    c.b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
-    c.c = big ? 1.0 : -0.0;
-    c.nm = big ? 0.0 : -1.0;
-    c.na = big ? -2.0 : -0.0;
-    c.k20 = ku << 20;
-    c.pad[0] = c.pad[1] = c.pad[2] = 0;
-#else
-    c.b_hi = far ? 0xbff00000u : 0x80000000u;
-    c.c_hi = big ? 0x3ff00000u : 0x80000000u;
-    c.k20 = ku << 20;
-    c.pad = 0;
-#endif
-    return c;
+    ea->x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
+    ea->x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
+    eb->b_hi = far ? 0xbff00000u : 0x80000000u;
+    eb->c_hi = big ? 0x3ff00000u : 0x80000000u;
+    eb->k20 = ku << 20;
+    eb->pad = 0;
 }
 
 // tanh_half_common with the class constants from `tab` (EXPM1_CLASSES
-// entries, tab[i] = expm1_class(i + EXPM1_K_MIN)).  Lanes outside the common
+// entries, entry i = expm1_class(i + EXPM1_K_MIN)).  Lanes outside the common
 // path (the callers' rare branch recomputes them) read a clamped entry.
 // k: s_expm1.c's explicit k = -1 for 0.5 ln2 < |u| < 1.5 ln2 (hi-word tests)
 // is what the rounded formula gives there anyway — only u < 0 reaches that
 // range, where invln2 * u - 0.5 lies in [-1.99999997, -1.00000001] — so only
 // the k = 0 test (|u| <= 0.5 ln2 by hi word) remains.  The result's sign:
 // the magnitude C + num / (y + 2) is > 0 on this path, so copysign by b.
-QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *tab) {
+QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     const double ln2_hi = 6.93147180369123816490e-01;
     const double ln2_lo = 1.90821492927058770002e-10;
     const double invln2 = 1.44269504088896338700e+00;
@@ -742,7 +731,8 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     int32_t k = (int32_t)kf;
     k = (ib > 0x3fd62e42u) ? k : 0;
     const int32_t kc = k < EXPM1_K_MIN ? EXPM1_K_MIN : (k > EXPM1_K_MAX ? EXPM1_K_MAX : k);
-    const Expm1Class cl = tab[kc - EXPM1_K_MIN];  // issued early, used after the division
+    const Expm1A ca = tab.a[kc - EXPM1_K_MIN];  // issued early, used after the division
+    const Expm1B cb = tab.b[kc - EXPM1_K_MIN];
     const double t = (double)k;
     const double hi = __builtin_fma(-t, ln2_hi, u);  // == u - t * ln2_hi: t * ln2_hi is exact (ln2_hi has 32 bits, |k| < 2^11)
     const double lo = t * ln2_lo;
@@ -759,19 +749,13 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, const Expm1Class *ta
     const double t3 = 3.0 - r1 * hfx;
     const double e = hxs * div_rn_safe(r1 - t3, 6.0 - xr * t3);
     const double e2 = (xr * (e - c) - c) - hxs;
-    const double ypre = (xr - (e2 + cl.x3)) + cl.x4;
+    const double ypre = (xr - (e2 + ca.x3)) + ca.x4;
     // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
     // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
     // end (round-to-nearest is symmetric; the sum is never 0 on this path).
-#if QL_CTAB == 64
-    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + cl.b;
-    const double num = __builtin_fma(y, cl.nm, cl.na);
-    const double zp = cl.c + div_rn_safe(num, y + 2.0);
-#else
-    const double y = with_hi_word(ypre, hi_word(ypre) + cl.k20) + from_words(cl.b_hi, 0u);
+    const double y = with_hi_word(ypre, hi_word(ypre) + cb.k20) + from_words(cb.b_hi, 0u);
     const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
-    const double zp = from_words(cl.c_hi, 0u) + div_rn_safe(num, y + 2.0);
-#endif
+    const double zp = from_words(cb.c_hi, 0u) + div_rn_safe(num, y + 2.0);
     *ib_out = ib;
     return __builtin_copysign(zp, b);
 }
@@ -810,7 +794,7 @@ QL_HD double tanh_half_clip(double b, double lim, double t_lim, int *tiny_or_nan
 }
 
 // tanh_half_clip on tanh_half_common_t (the table form).
-QL_HD double tanh_half_clip_t(double b, double lim, double t_lim, int *tiny_or_nan, const Expm1Class *tab) {
+QL_HD double tanh_half_clip_t(double b, double lim, double t_lim, int *tiny_or_nan, Expm1Tab tab) {
     uint32_t ib;
     double z = tanh_half_common_t(b, &ib, tab);
     const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) frame_weight_kernel(int n, int m, const i
                                                            const int32_t *row_deg, const uint8_t *synd,
                                                            const double *llr, const uint8_t *codes,
                                                            const double *palette, const uint8_t *pal_ok,
-                                                           int32_t *weight) {
+                                                           const int32_t *col_orig, int32_t *weight) {
     extern __shared__ uint32_t zmask[];
     const size_t f = blockIdx.x;
     const int nw = (n + 31) / 32;
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(256) frame_weight_kernel(int n, int m, const i
             const double *l = llr + f * (size_t)n;
             for (int s = 0; s < 32; ++s) {
                 const int i = wd * 32 + s;
-                if (i < n && l[i] <= 0.0) z |= 1u << s;
+                if (i < n && l[col_orig ? col_orig[i] : i] <= 0.0) z |= 1u << s;  // (bit i of z: label i)
             }
         }
         zmask[wd] = z;
@@ -135,10 +135,14 @@ size_t frame_weight_lds(int n) { return (size_t)((n + 31) / 32) * 4; }
 hipError_t launch_frame_order(int n, int m, const int32_t *ell_col, const int32_t *row_deg, int batch,
                               const uint8_t *synd, const double *llr, const uint8_t *codes,
                               const double *palette, const uint8_t *pal_ok, int32_t *weight, int32_t *order,
-                              hipStream_t stream) {
+                              const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
+    // (n near 2^20 needs up to 128 KiB of dynamic LDS: opt in like every large-LDS launch)
+    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void *>(frame_weight_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)frame_weight_lds(n));
+    if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(frame_weight_kernel, dim3(batch), dim3(256), frame_weight_lds(n), stream, n, m, ell_col,
-                       row_deg, synd, llr, codes, palette, pal_ok, weight);
+                       row_deg, synd, llr, codes, palette, pal_ok, col_orig, weight);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(frame_order_kernel, dim3(1), dim3(ORDER_THREADS), 0, stream, batch, weight, order);

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, cons
                                                               const uint8_t *palice, const uint8_t *pbob,
                                                               const double *log_p, uint8_t *alice_ext, double *llr,
                                                               uint8_t *synd, uint8_t *codes, double *palette,
-                                                              uint8_t *pal_ok) {
+                                                              uint8_t *pal_ok, const int32_t *col_orig) {
     const size_t f = blockIdx.x;
     const double lp = log_p[f];
     const uint8_t *al = alice + f * (size_t)n;
@@ -191,8 +191,10 @@ __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, cons
         uint8_t *cs = codes + f * (size_t)nc;
         for (int j = threadIdx.x; j < nc; j += blockDim.x) {
             int byte = 0;
-            for (int q = 0; q < 4; ++q)
-                if (4 * j + q < n) byte |= bob_code(4 * j + q) << (2 * q);
+            for (int q = 0; q < 4; ++q) {  // label order (col_orig)
+                const int i = 4 * j + q;
+                if (i < n) byte |= bob_code(col_orig ? col_orig[i] : i) << (2 * q);
+            }
             cs[j] = (uint8_t)byte;
         }
         if (threadIdx.x < 4) {
@@ -217,10 +219,11 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
                                   const int32_t *src, int n_punct, int batch, const uint8_t *alice, const uint8_t *bob,
                                   const uint8_t *palice, const uint8_t *pbob, const double *log_p, uint8_t *alice_ext,
                                   double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
-                                  hipStream_t stream) {
+                                  const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, cls, src,
-                       n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok);
+                       n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok,
+                       col_orig);
     return hipGetLastError();
 }
 

@@ -91,16 +91,38 @@ class DecodeOutput:
 
 
 class Graph:
-    """A device-resident Tanner graph (qldpc_graph)."""
+    """A device-resident Tanner graph (qldpc_graph).
 
-    def __init__(self, H: HMatrix, device_mask: int = 0):
+    device_mask: replicate on these HIP devices (bit d = device d; 0 = the
+    current one).  devices: an explicit list instead, one shard per entry
+    (a device may repeat: concurrent shards on one GPU); decode() then splits a
+    batch in len(devices) contiguous slices, one host thread each.
+    host_only: plan without touching a device (inspection; cannot decode)."""
+
+    def __init__(self, H: HMatrix, device_mask: int = 0, devices=None, host_only: bool = False):
         self.H = H
         self.n, self.m = H.n, H.m
         g = ctypes.c_void_p()
-        check(lib().qldpc_graph_create_checked(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(H.col_ptr),
-                                               ptr(H.row_idx), int(device_mask), ctypes.byref(g)),
-              "qldpc_graph_create_checked")
+        if host_only:
+            check(lib().qldpc_graph_create_host(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ctypes.byref(g)),
+                  "qldpc_graph_create_host")
+        elif devices is not None:
+            dl = np.ascontiguousarray(devices, np.int32)
+            check(lib().qldpc_graph_create_on(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(dl), int(dl.size),
+                                              ctypes.byref(g)), "qldpc_graph_create_on")
+        else:
+            check(lib().qldpc_graph_create_checked(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(H.col_ptr),
+                                                   ptr(H.row_idx), int(device_mask), ctypes.byref(g)),
+                  "qldpc_graph_create_checked")
         self._g = g
+
+    def labels(self) -> tuple[np.ndarray, dict]:
+        """The decoder's bank-aware label of each bit id, and the relabelling stats."""
+        lab = np.empty(self.n, np.int32)
+        st = np.zeros(4, np.int64)
+        check(lib().qldpc_graph_labels(self._g, ptr(lab), ptr(st)), "qldpc_graph_labels")
+        return lab, {"excess_before": int(st[0]), "excess_after": int(st[1]), "cycles_before": int(st[2]),
+                     "cycles_after": int(st[3])}
 
     @property
     def handle(self) -> ctypes.c_void_p:
@@ -130,6 +152,17 @@ class Graph:
                                      ctypes.byref(wgs), ctypes.byref(lds), ctypes.byref(var)), "qldpc_graph_plan")
         return {"lanes": lanes.value, "edges_per_lane": epl.value, "workgroups": wgs.value,
                 "lds_bytes": lds.value, "variant": var.value.decode()}
+
+    def set_kernel_timing(self, enabled: bool = True) -> None:
+        """Bracket every decode kernel launch with HIP events (qldpc_set_kernel_timing)."""
+        check(lib().qldpc_set_kernel_timing(self._g, 1 if enabled else 0), "qldpc_set_kernel_timing")
+
+    def last_decode_kernel_ms(self, stream=None, device: int = 0) -> float:
+        """Duration of the last timed decode kernel on (device, stream); waits for it."""
+        ms = ctypes.c_float(0.0)
+        check(lib().qldpc_last_decode_kernel_ms(self._g, device, _stream_ptr(stream, device), ctypes.byref(ms)),
+              "qldpc_last_decode_kernel_ms")
+        return float(ms.value)
 
     # ---- host-buffer decode (synchronous, shards over the graph's devices) ----
     def decode(self, params: Params, llr: np.ndarray, syndrome: np.ndarray, posterior: bool = False) -> DecodeOutput:

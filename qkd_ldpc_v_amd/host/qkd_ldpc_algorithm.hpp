@@ -1,31 +1,32 @@
-// qkd_ldpc_algorithm.hpp — C++ mirror of the reference's decode interface,
-// backed by libqkdldpc_hip.so (include/qkd_ldpc_hip.h).
+// qkd_ldpc_algorithm.hpp — C++ mirror of the reference's decode interface in
+// namespace qkd_ldpc_v_amd, backed by libqkdldpc_hip.so (include/qkd_ldpc_hip.h).
 //
 // Same names, argument meaning and error behaviour as ColdCloudd/QKD_LDPC_V:
-//   H_matrix                  src/array_and_matrix_operations.hpp:60-77
+//   H_matrix, H_matrix_params src/array_and_matrix_operations.hpp:27-77
 //   read_sparse_*             src/array_and_matrix_operations.cpp:291-886
-//   decoding_result, LDPC_result, the six decoders, QKD_LDPC
-//                             src/qkd_ldpc_algorithm.hpp:16-99
+//   decoding_result, LDPC_result, the six decoders, tanh/atanh_lin_approx,
+//   QKD_LDPC, QKD_LDPC_RATE_ADAPT
+//                             src/qkd_ldpc_algorithm.hpp:16-109
 //   calculate_syndrome, arrays_equal, remove_bits
 //                             src/array_and_matrix_operations.cpp:105-118,259-287,936-950
 //   config_data / CFG (the subset the hot path reads)   src/config.hpp:103-198
-// A caller of the reference switches by including this header instead: every
-// decoder call runs on the GPU.  decode_batch() is the batched entry a driver
-// uses in place of the per-trial thread pool (src/simulation.cpp:740-746).
+// For a program that includes this header instead of the reference's.  The
+// drop-in for the reference's OWN build — its globals, its H_matrix, its
+// generator type — is dropin/qkd_ldpc_algorithm.cpp; both
+// are thin layers over qkd_ldpc_impl.hpp.  decode_batch() is the batched entry
+// a driver uses in place of the per-trial thread pool (src/simulation.cpp:740-746).
 // Errors are std::runtime_error carrying qldpc_last_error().
 #pragma once
 
 #include <cmath>
 #include <cstdint>
 #include <filesystem>
-#include <map>
-#include <memory>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "qkd_ldpc_hip.h"
+#include "qkd_ldpc_impl.hpp"
 
 namespace qkd_ldpc_v_amd {
 
@@ -72,10 +73,6 @@ struct LDPC_result {
 
 namespace detail {
 
-[[noreturn]] inline void raise(const char *what) {
-    throw std::runtime_error(std::string(what) + ": " + qldpc_last_error());
-}
-
 inline H_matrix load(const std::filesystem::path &p, int32_t format) {
     int32_t n = 0, m = 0, nnz = 0, reg = 0;
     if (qldpc_load_matrix(p.c_str(), format, &n, &m, &nnz, nullptr, nullptr, nullptr, nullptr, &reg))
@@ -92,54 +89,17 @@ inline H_matrix load(const std::filesystem::path &p, int32_t format) {
     return H;
 }
 
-// One device graph per distinct H (keyed by address + shape; the reference
-// passes the same const H_matrix& to every trial).
-struct GraphCache {
-    std::mutex mu;
-    std::map<const H_matrix *, std::pair<size_t, std::shared_ptr<qldpc_graph>>> graphs;
+inline impl::DecodeConfig cfg() {
+    return {(int32_t)CFG.DECODING_ALGORITHM, CFG.DECODING_ALG_MAX_ITERATIONS, CFG.ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD,
+            CFG.DECODING_ALG_MSG_LLR_THRESHOLD};
+}
 
-    std::shared_ptr<qldpc_graph> get(const H_matrix &H) {
-        size_t nnz = 0;
-        for (const auto &r : H.check_nodes) nnz += r.size();
-        const size_t key = H.bit_nodes.size() * 1000003u ^ H.check_nodes.size() * 7919u ^ nnz;
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = graphs.find(&H);
-        if (it != graphs.end() && it->second.first == key) return it->second.second;
-        std::vector<int32_t> rp(H.check_nodes.size() + 1, 0), ci, cp(H.bit_nodes.size() + 1, 0), ri;
-        for (size_t j = 0; j < H.check_nodes.size(); ++j) {
-            ci.insert(ci.end(), H.check_nodes[j].begin(), H.check_nodes[j].end());
-            rp[j + 1] = (int32_t)ci.size();
-        }
-        for (size_t i = 0; i < H.bit_nodes.size(); ++i) {
-            ri.insert(ri.end(), H.bit_nodes[i].begin(), H.bit_nodes[i].end());
-            cp[i + 1] = (int32_t)ri.size();
-        }
-        qldpc_graph *g = nullptr;
-        if (qldpc_graph_create_checked((int32_t)H.bit_nodes.size(), (int32_t)H.check_nodes.size(), rp.data(),
-                                       ci.data(), cp.data(), ri.data(), 0, &g))
-            raise("qldpc_graph_create_checked");
-        std::shared_ptr<qldpc_graph> sp(g, qldpc_graph_destroy);
-        graphs[&H] = {key, sp};
-        return sp;
-    }
-};
-inline GraphCache graph_cache;
-
-inline decoding_result decode_one(int32_t alg, const std::vector<double> &llr, const H_matrix &H,
-                                  const std::vector<int> &syndrome, size_t max_it, double primary, double secondary,
-                                  double thr, std::vector<int> &out) {
-    auto g = graph_cache.get(H);
-    const size_t n = H.bit_nodes.size(), m = H.check_nodes.size();
-    std::vector<uint8_t> s(m), bits(n);
-    for (size_t j = 0; j < m; ++j) s[j] = (uint8_t)(syndrome[j] & 1);
-    qldpc_params p{alg, (int32_t)max_it, CFG.ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD ? 1 : 0, 0, thr, primary, secondary};
-    uint32_t iters = 0;
-    uint8_t ok = 0;
-    if (qldpc_decode_batch(g.get(), &p, 1, llr.data(), s.data(), bits.data(), &iters, &ok, nullptr))
-        raise("qldpc_decode_batch");
-    out.resize(n);
-    for (size_t i = 0; i < n; ++i) out[i] = bits[i];
-    return {iters, ok != 0};
+inline decoding_result decode(int32_t alg, const std::vector<double> &llr, const H_matrix &H,
+                              const std::vector<int> &syndrome, size_t max_it, double primary, double secondary,
+                              double thr, std::vector<int> &out) {
+    const auto r = impl::decode_one(alg, llr, H, syndrome, max_it, primary, secondary,
+                                    CFG.ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD, thr, out);
+    return {r.first, r.second};
 }
 
 }  // namespace detail
@@ -153,102 +113,86 @@ inline H_matrix read_sparse_matrix_2(const std::filesystem::path &p) { return de
 // ---- array helpers ---------------------------------------------------------
 inline void calculate_syndrome(const std::vector<int> &bit_array, const H_matrix &matrix,
                                std::vector<int> &syndrome_out) {
-    std::fill(syndrome_out.begin(), syndrome_out.end(), 0);
-    for (size_t i = 0; i < matrix.check_nodes.size(); ++i)
-        for (int b : matrix.check_nodes[i]) syndrome_out[i] ^= bit_array[b];
+    impl::calculate_syndrome(bit_array, matrix, syndrome_out);
 }
-
-inline bool arrays_equal(const std::vector<int> &a, const std::vector<int> &b) {
-    for (size_t i = 0; i < a.size(); ++i)
-        if (a[i] != b[i]) return false;
-    return true;
-}
-
+inline bool arrays_equal(const std::vector<int> &a, const std::vector<int> &b) { return impl::arrays_equal(a, b); }
 inline void remove_bits(const std::vector<int> &bits_to_remove, const std::vector<int> &array1,
                         const std::vector<int> &array2, std::vector<int> &array1_out, std::vector<int> &array2_out) {
-    const size_t btr = bits_to_remove.size();
-    array1_out.resize(array1.size() - btr);
-    array2_out.resize(array1.size() - btr);
-    size_t n = 0, m = 0;
-    for (size_t i = 0; i < array1.size(); ++i) {
-        if (n < btr && bits_to_remove[n] == (int)i) {
-            ++n;
-        } else {
-            array1_out[m] = array1[i];
-            array2_out[m] = array2[i];
-            ++m;
-        }
-    }
+    impl::remove_bits(bits_to_remove, array1, array2, array1_out, array2_out);
 }
 
-// ---- the six decoders (src/qkd_ldpc_algorithm.hpp:28-90) -------------------
+// ---- the six decoders and the linear approximations (src/qkd_ldpc_algorithm.hpp:28-90)
 inline decoding_result sum_product_decoding(const std::vector<double> &bit_array_llr, const H_matrix &matrix,
                                             const std::vector<int> &syndrome, const size_t &max_num_iterations,
                                             const double &msg_threshold, std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_SPA, bit_array_llr, matrix, syndrome, max_num_iterations, 0, 0, msg_threshold,
-                              bit_array_out);
+    return detail::decode(QLDPC_SPA, bit_array_llr, matrix, syndrome, max_num_iterations, 0, 0, msg_threshold,
+                          bit_array_out);
 }
+inline double tanh_lin_approx(double x) { return impl::tanh_lin_approx(x); }
+inline double atanh_lin_approx(double x) { return impl::atanh_lin_approx(x); }
 inline decoding_result sum_product_linear_approx_decoding(const std::vector<double> &bit_array_llr,
                                                           const H_matrix &matrix, const std::vector<int> &syndrome,
                                                           const size_t &max_num_iterations,
                                                           const double &msg_threshold,
                                                           std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_SPA_LIN, bit_array_llr, matrix, syndrome, max_num_iterations, 0, 0,
-                              msg_threshold, bit_array_out);
+    return detail::decode(QLDPC_SPA_LIN, bit_array_llr, matrix, syndrome, max_num_iterations, 0, 0, msg_threshold,
+                          bit_array_out);
 }
 inline decoding_result min_sum_normalized_decoding(const std::vector<double> &bit_array_llr, const H_matrix &matrix,
                                                    const std::vector<int> &syndrome, const size_t &max_num_iterations,
                                                    const double &alpha, const double &msg_threshold,
                                                    std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_NMSA, bit_array_llr, matrix, syndrome, max_num_iterations, alpha, 0,
-                              msg_threshold, bit_array_out);
+    return detail::decode(QLDPC_NMSA, bit_array_llr, matrix, syndrome, max_num_iterations, alpha, 0, msg_threshold,
+                          bit_array_out);
 }
 inline decoding_result min_sum_offset_decoding(const std::vector<double> &bit_array_llr, const H_matrix &matrix,
                                                const std::vector<int> &syndrome, const size_t &max_num_iterations,
                                                const double &beta, const double &msg_threshold,
                                                std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_OMSA, bit_array_llr, matrix, syndrome, max_num_iterations, beta, 0,
-                              msg_threshold, bit_array_out);
+    return detail::decode(QLDPC_OMSA, bit_array_llr, matrix, syndrome, max_num_iterations, beta, 0, msg_threshold,
+                          bit_array_out);
 }
 inline decoding_result adaptive_min_sum_normalized_decoding(const std::vector<double> &bit_array_llr,
                                                             const H_matrix &matrix, const std::vector<int> &syndrome,
                                                             const size_t &max_num_iterations, const double &alpha,
                                                             const double &nu, const double &msg_threshold,
                                                             std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_ANMSA, bit_array_llr, matrix, syndrome, max_num_iterations, alpha, nu,
-                              msg_threshold, bit_array_out);
+    return detail::decode(QLDPC_ANMSA, bit_array_llr, matrix, syndrome, max_num_iterations, alpha, nu, msg_threshold,
+                          bit_array_out);
 }
 inline decoding_result adaptive_min_sum_offset_decoding(const std::vector<double> &bit_array_llr,
                                                         const H_matrix &matrix, const std::vector<int> &syndrome,
                                                         const size_t &max_num_iterations, const double &beta,
                                                         const double &sigma, const double &msg_threshold,
                                                         std::vector<int> &bit_array_out) {
-    return detail::decode_one(QLDPC_AOMSA, bit_array_llr, matrix, syndrome, max_num_iterations, beta, sigma,
-                              msg_threshold, bit_array_out);
+    return detail::decode(QLDPC_AOMSA, bit_array_llr, matrix, syndrome, max_num_iterations, beta, sigma,
+                          msg_threshold, bit_array_out);
 }
 
-// ---- per-trial entry (src/qkd_ldpc_algorithm.cpp:1031-1119) ---------------
+// ---- per-trial entries (src/qkd_ldpc_algorithm.cpp:1031-1258) --------------
 inline LDPC_result QKD_LDPC(const H_matrix &matrix, const std::vector<int> &alice_bit_array,
                             const std::vector<int> &bob_bit_array, const double &QBER,
                             const decoding_scaling_factors &scaling_factors = {},
                             const H_matrix_params &matrix_params = {}) {
-    const size_t n = matrix.bit_nodes.size(), m = matrix.check_nodes.size();
-    const double log_p = std::log((1. - QBER) / QBER);
-    std::vector<double> apriori_llr(n);
-    for (size_t i = 0; i < n; ++i) apriori_llr[i] = bob_bit_array[i] ? -log_p : log_p;
-    std::vector<int> alice_syndrome(m);
-    calculate_syndrome(alice_bit_array, matrix, alice_syndrome);
-    std::vector<int> bob_solution(n);
-    LDPC_result r;
-    r.decoding_res = detail::decode_one((int32_t)CFG.DECODING_ALGORITHM, apriori_llr, matrix, alice_syndrome,
-                                        CFG.DECODING_ALG_MAX_ITERATIONS, scaling_factors.primary,
-                                        scaling_factors.secondary, CFG.DECODING_ALG_MSG_LLR_THRESHOLD, bob_solution);
-    r.keys_match = arrays_equal(alice_bit_array, bob_solution);
-    if (CFG.ENABLE_PRIVACY_MAINTENANCE) {
-        std::vector<int> a_pm, b_pm;
-        remove_bits(matrix_params.bits_to_remove, alice_bit_array, bob_solution, a_pm, b_pm);
-    }
-    return r;
+    (void)matrix_params;  // privacy maintenance's remove_bits only feeds the reference's TRACE output
+    const auto r = impl::qkd_ldpc(matrix, alice_bit_array, bob_bit_array, QBER, scaling_factors.primary,
+                                  scaling_factors.secondary, detail::cfg());
+    return {{r.iterations_num, r.syndromes_match}, r.keys_match};
+}
+
+// The reference takes XoshiroCpp::Xoshiro256PlusPlus&; any uniform random bit
+// generator binds here, and its draws are consumed exactly as there (two
+// uniform_int_distribution<int>(0, 1) draws per punctured position, in
+// position order).
+template <class URBG>
+LDPC_result QKD_LDPC_RATE_ADAPT(const H_matrix &matrix, const std::vector<int> &alice_bit_array,
+                                const std::vector<int> &bob_bit_array, const double &QBER,
+                                const decoding_scaling_factors &scaling_factors, const H_matrix_params &matrix_params,
+                                URBG &prng) {
+    const auto r = impl::qkd_ldpc_rate_adapt(matrix, alice_bit_array, bob_bit_array, QBER, scaling_factors.primary,
+                                             scaling_factors.secondary, matrix_params.punctured_bits,
+                                             matrix_params.shortened_bits, prng, detail::cfg());
+    return {{r.iterations_num, r.syndromes_match}, r.keys_match};
 }
 
 // ---- batched entry for drivers ---------------------------------------------
@@ -257,8 +201,10 @@ inline std::vector<decoding_result> decode_batch(const H_matrix &matrix, const s
                                                  const std::vector<uint8_t> &syndrome, size_t batch,
                                                  const decoding_scaling_factors &sf,
                                                  std::vector<uint8_t> &bits_out) {
-    auto g = detail::graph_cache.get(matrix);
-    const size_t n = matrix.bit_nodes.size();
+    auto g = impl::graph_cache().get(matrix);
+    const size_t n = matrix.bit_nodes.size(), m = matrix.check_nodes.size();
+    if (llr.size() < batch * n || syndrome.size() < batch * m)
+        throw std::runtime_error("decode_batch: llr / syndrome shorter than batch frames");
     bits_out.resize(batch * n);
     std::vector<uint32_t> it(batch);
     std::vector<uint8_t> ok(batch);
@@ -267,10 +213,14 @@ inline std::vector<decoding_result> decode_batch(const H_matrix &matrix, const s
                    sf.primary, sf.secondary};
     if (qldpc_decode_batch(g.get(), &p, (int32_t)batch, llr.data(), syndrome.data(), bits_out.data(), it.data(),
                            ok.data(), nullptr))
-        detail::raise("qldpc_decode_batch");
+        impl::raise("qldpc_decode_batch");
     std::vector<decoding_result> res(batch);
     for (size_t f = 0; f < batch; ++f) res[f] = {it[f], ok[f] != 0};
     return res;
 }
+
+// Device graphs are cached by H content; free one (or all) explicitly.
+inline bool release_matrix(const H_matrix &matrix) { return impl::graph_cache().release(matrix); }
+inline void release_all_matrices() { impl::graph_cache().clear(); }
 
 }  // namespace qkd_ldpc_v_amd

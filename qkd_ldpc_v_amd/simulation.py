@@ -378,40 +378,41 @@ def prepare(cfg: Config, matrix_paths: list[str]):
 
 
 # ---- trials on the GPU + statistics -------------------------------------------
-def run(cfg: Config, mats, combos, device: int = 0, max_batch: int = 4096, log=print):
+def shard_ranges(total: int, shards: int) -> list[tuple[int, int]]:
+    """Contiguous trial slices [b, e) of ceil(total / shards) trials, one per
+    shard; trailing shards may be short or empty."""
+    shards = max(1, int(shards))
+    per = -(-total // shards)
+    return [(min(total, k * per), min(total, (k + 1) * per)) for k in range(shards)]
+
+
+def _run_shard(cfg, H, c, sim, p, graph, plan, dev, stream, seeds, b, e, max_batch):
+    """Trials [b, e) of one combination on one device/stream: run_trial's keys
+    (device generator), then QKD_LDPC[_RATE_ADAPT]'s window (fused entry).
+    -> (iterations, syndromes_match, keys_match, accurate_qber, seconds in the window)."""
     import torch
 
-    dev = torch.device("cuda", device)
-    torch.cuda.set_device(dev)
-    seeds = trial_seeds(cfg.simulation_seed, cfg.trials_number)
-    graphs = {}
-    results = []
-    for sim, c in enumerate(combos):
-        path, H = mats[c.matrix_index]
-        g = graphs.get(c.matrix_index) or graphs.setdefault(c.matrix_index, Graph(H))
-        p = Params(cfg.decoding_algorithm, cfg.max_iterations, cfg.threshold_enabled, cfg.threshold, c.primary,
-                   c.secondary)
-        ra = c.punctured is not None
-        plan = g.rate_plan(c.punctured, c.shortened) if ra else None
-        it_all, ok_all, km_all = [], [], []
-        t_pipe = 0.0
-        q_acc = None
-        for b0 in range(0, cfg.trials_number, max_batch):
-            nb = min(max_batch, cfg.trials_number - b0)
+    from .graph import trials_device, trials_rate_adapt_device
+
+    ra = c.punctured is not None
+    it_all, ok_all, km_all = [], [], []
+    t_pipe = 0.0
+    q_acc = None
+    with torch.cuda.device(dev), torch.cuda.stream(stream):
+        for b0 in range(b, e, max_batch):
+            nb = min(max_batch, e - b0)
             ds = torch.from_numpy(seeds[b0:b0 + nb].view(np.int64)).to(dev)
             ta = torch.empty((nb, H.n), dtype=torch.uint8, device=dev)
             tb = torch.empty_like(ta)
             np_ = max(1, c.punctured.size) if ra else 1
             pa = torch.empty((nb, np_), dtype=torch.uint8, device=dev)
             pb = torch.empty_like(pa)
-            from .graph import trials_device, trials_rate_adapt_device
-
             # trial seed = seeds[n] + curr_sim (src/simulation.cpp:743)
             if ra:
                 q_acc = trials_rate_adapt_device(H.n, c.config_qber, ds, c.punctured.size, ta, tb, pa, pb,
-                                                 seed_add=sim)
+                                                 seed_add=sim, stream=stream)
             else:
-                q_acc = trials_device(H.n, c.config_qber, ds, ta, tb, seed_add=sim)
+                q_acc = trials_device(H.n, c.config_qber, ds, ta, tb, seed_add=sim, stream=stream)
             lp = torch.full((nb,), log_p(q_acc), dtype=torch.float64, device=dev)  # the C library's log (:1043)
             llr = torch.empty((nb, H.n), dtype=torch.float64, device=dev)
             syn = torch.empty((nb, H.m), dtype=torch.uint8, device=dev)
@@ -419,21 +420,85 @@ def run(cfg: Config, mats, combos, device: int = 0, max_batch: int = 4096, log=p
             it = torch.empty(nb, dtype=torch.int32, device=dev)
             ok = torch.empty(nb, dtype=torch.uint8, device=dev)
             km = torch.empty(nb, dtype=torch.uint8, device=dev)
-            torch.cuda.synchronize()
+            stream.synchronize()
             t0 = time.perf_counter()
             if ra:
                 ax = torch.empty_like(ta)
-                g.qkd_ldpc_rate_adapt_device(plan, p, ta, tb, pa, pb, lp, ax, llr, syn, bits, it, ok, km)
+                graph.qkd_ldpc_rate_adapt_device(plan, p, ta, tb, pa, pb, lp, ax, llr, syn, bits, it, ok, km,
+                                                 stream=stream)
             else:
-                g.qkd_ldpc_device(p, ta, tb, lp, llr, syn, bits, it, ok, km)
-            torch.cuda.synchronize()
+                graph.qkd_ldpc_device(p, ta, tb, lp, llr, syn, bits, it, ok, km, stream=stream)
+            stream.synchronize()
             t_pipe += time.perf_counter() - t0
             it_all.append(it.cpu().numpy())
             ok_all.append(ok.cpu().numpy())
             km_all.append(km.cpu().numpy())
-        it = np.concatenate(it_all).astype(np.int64)
-        ok = np.concatenate(ok_all).astype(bool)
-        km = np.concatenate(km_all).astype(bool)
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+    return cat(it_all, np.int64), cat(ok_all, bool), cat(km_all, bool), q_acc, t_pipe
+
+
+def run(cfg: Config, mats, combos, device: int = 0, max_batch: int = 4096, log=print, devices=None):
+    """The simulation loop over combinations (src/simulation.cpp:700-760).
+
+    devices: the GPUs to shard each combination's trials over (default
+    [device]).  The reference runs TRIALS_NUMBER trials of a combination on a
+    thread pool (:721,740-746); here the trial range is split in contiguous
+    slices, one per entry of `devices`, each decoded by its own host thread on
+    its own stream and graph replica, with no collective: the per-trial
+    results are concatenated in trial order on the host before the statistics
+    (process_trials_results, :580-690).  An entry may repeat a device (several
+    concurrent shards on one GPU).  The statistics do not depend on the
+    sharding: every trial's result is a function of its seed alone."""
+    import threading
+
+    import torch
+
+    devs = [int(d) for d in (devices if devices else [device])]
+    torch.cuda.set_device(devs[0])
+    streams = [torch.cuda.Stream(torch.device("cuda", d)) for d in devs]
+    seeds = trial_seeds(cfg.simulation_seed, cfg.trials_number)
+    graphs = {}  # (matrix, device) -> Graph replica
+    results = []
+    for sim, c in enumerate(combos):
+        path, H = mats[c.matrix_index]
+        p = Params(cfg.decoding_algorithm, cfg.max_iterations, cfg.threshold_enabled, cfg.threshold, c.primary,
+                   c.secondary)
+        ra = c.punctured is not None
+        gp = {}
+        for d in sorted(set(devs)):
+            key = (c.matrix_index, d)
+            if key not in graphs:
+                with torch.cuda.device(d):
+                    graphs[key] = Graph(H)
+            gp[d] = (graphs[key], graphs[key].rate_plan(c.punctured, c.shortened) if ra else None)
+        ranges = shard_ranges(cfg.trials_number, len(devs))
+        outs = [None] * len(devs)
+        errs = []
+
+        def work(k):
+            try:
+                d = devs[k]
+                g, plan = gp[d]
+                outs[k] = _run_shard(cfg, H, c, sim, p, g, plan, torch.device("cuda", d), streams[k], seeds,
+                                     ranges[k][0], ranges[k][1], max_batch)
+            except BaseException as e:  # reported after the join, like the C ABI's per-device errors
+                errs.append(e)
+
+        if len(devs) == 1:
+            work(0)
+        else:
+            th = [threading.Thread(target=work, args=(k,)) for k in range(len(devs))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errs:
+            raise errs[0]
+        it = np.concatenate([o[0] for o in outs])
+        ok = np.concatenate([o[1] for o in outs])
+        km = np.concatenate([o[2] for o in outs])
+        q_acc = next(o[3] for o in outs if o[3] is not None)
+        t_pipe = max(o[4] for o in outs)  # shards run concurrently
         r = _stats(cfg, sim, os.path.basename(path), H, c, q_acc, it, ok, km, t_pipe)
         results.append(r)
         log(f"[{sim + 1}/{len(combos)}] {r['matrix_filename']} QBER={c.config_qber:.4f} "
@@ -534,14 +599,17 @@ def main(argv=None) -> int:
     ap.add_argument("--matrices", required=True, help="directory of *.mtrx files in the config's matrix_format")
     ap.add_argument("--results", default="results")
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="shard every combination's trials over GPUs 0..N-1 of this node (0: --device only)")
     a = ap.parse_args(argv)
+    devices = list(range(a.gpus)) if a.gpus > 0 else [a.device]
     for i, cp in enumerate(a.configs):
         cfg = Config.load(cp)
         print(f"CONFIG #{i + 1}: {os.path.basename(cp)} — {DEC_NAMES[cfg.decoding_algorithm]}, "
               f"{cfg.trials_number} trials, seed {cfg.simulation_seed}")
         mats, combos = prepare(cfg, matrix_files(a.matrices))
         t0 = time.time()
-        res = run(cfg, mats, combos, device=a.device)
+        res = run(cfg, mats, combos, devices=devices)
         dt = int(time.time() - t0)
         dur = f"{dt // 3600:02d}h-{dt % 3600 // 60:02d}m-{dt % 60:02d}s"
         print("The results are written to the file:", write_results(cfg, res, dur, a.results))

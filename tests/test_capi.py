@@ -52,3 +52,48 @@ def test_graph_rejects_inconsistent_edges():
     bad.col_ptr[-1] -= 1
     with pytest.raises(QLDPCError):
         Q.Graph(bad)
+
+
+def test_atomic_optimizer_workaround_on_every_product_compile():
+    """The split-frame miscompile workaround (Makefile comment)
+    must reach every hipcc line of the product library."""
+    mk = open(os.path.join(ROOT, "Makefile")).read()
+    hipflags = re.search(r"^HIPFLAGS := (.*?)(?<!\\)\n", mk, flags=re.S | re.M).group(1)
+    assert "-amdgpu-atomic-optimizer-strategy=None" in hipflags
+    for line in mk.splitlines():
+        if line.strip().startswith("$(HIPCC)") and " -c " in line:
+            assert "$(HIPFLAGS)" in line, line
+
+
+def test_bank_relabelling_host_plan():
+    """The planner's bank-aware bit labels (relabel.cpp), host only: a
+    permutation, deterministic, and on the random 10k codes it drives every
+    slot group's busiest LDS bank down (C2: 3.5 -> about 2 addresses per half)."""
+    from conftest import load_fixture
+
+    for name in ("c2_n10240_m2201.alist", "c3_n10240_m1801.alist"):
+        H = load_fixture(name)
+        lab, st = Q.Graph(H, host_only=True).labels()
+        assert np.array_equal(np.sort(lab), np.arange(H.n))
+        assert st["cycles_after"] < 0.7 * st["cycles_before"], st
+        assert st["excess_after"] < st["excess_before"]
+        lab2, _ = Q.Graph(H, host_only=True).labels()
+        assert np.array_equal(lab, lab2)
+
+
+def test_relabelling_only_on_one_workgroup_register_shapes():
+    from conftest import load_fixture
+
+    H = load_fixture("c4s_n102400_m32001.alist")  # split frames: reference ids
+    lab, st = Q.Graph(H, host_only=True).labels()
+    assert np.array_equal(lab, np.arange(H.n)) and st["cycles_before"] == 0
+    old = os.environ.get("QLDPC_RELABEL")
+    os.environ["QLDPC_RELABEL"] = "0"
+    try:
+        lab, _ = Q.Graph(load_fixture("c2_n10240_m2201.alist"), host_only=True).labels()
+        assert np.array_equal(lab, np.arange(lab.size))
+    finally:
+        if old is None:
+            os.environ.pop("QLDPC_RELABEL")
+        else:
+            os.environ["QLDPC_RELABEL"] = old

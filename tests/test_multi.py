@@ -65,3 +65,72 @@ def test_single_rank_combine_without_dist():
 
     tot = bench.combine_ranks(None, 3.0, 5, 4, 4, 4, 1.5, torch.device("cpu"))
     assert tot == {"elapsed_max": 3.0, "kernel_ms_max": 1.5, "iters": 5.0, "ok": 4.0, "keys": 4.0, "frames": 4.0}
+
+
+# ---- device sharding in the product ---------------------------
+def test_shard_ranges_contiguous_and_complete():
+    from qkd_ldpc_v_amd.simulation import shard_ranges
+
+    for total, shards in [(4097, 3), (10, 1), (2, 3), (0, 2), (4096, 8), (7, 7)]:
+        r = shard_ranges(total, shards)
+        assert len(r) == shards
+        assert r[0][0] == 0 and r[-1][1] == total
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:])), "slices must be contiguous"
+        per = -(-total // shards)
+        assert all(0 <= e - b <= per for b, e in r)
+
+
+@pytest.mark.gpu
+def test_decode_batch_logical_shards_match_oracle(gpu_available):
+    """qldpc_decode_batch's multi-device branch — one host thread, stream and
+    graph replica per shard, contiguous uneven slices, per-shard error
+    collection — exercised with G = 3 logical shards on device 0 and an uneven
+    batch of 4097 frames, against the oracle and the single-shard decode."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import qkd_ldpc_v_amd as Q
+    from conftest import load_fixture
+    from oracle.pyoracle import Oracle
+
+    H = load_fixture("c1_n1024_m220.alist")
+    a, b, q = Q.bsc_frames(H.n, 0.03, 4097, seed=31)
+    lp = Q.log_p(q)
+    llr = np.where(b != 0, -lp, lp).astype(np.float64)
+    s = H.syndrome(a)
+    p = Q.Params(Q.SPA, 50, True, 100.0)
+    g3 = Q.Graph(H, devices=[0, 0, 0])
+    assert g3.info()["devices"] == 3
+    out3 = g3.decode(p, llr, s, posterior=True)
+    out1 = Q.Graph(H).decode(p, llr, s, posterior=True)
+    assert np.array_equal(out3.bits, out1.bits) and np.array_equal(out3.iterations, out1.iterations)
+    assert np.array_equal(out3.posterior.view(np.uint64), out1.posterior.view(np.uint64))
+    O = Oracle(H)
+    ob, oi, ok, _ = O.decode_batch(O.params(Q.SPA, 50, True, 100.0), llr, s, threads=16)
+    assert np.array_equal(out3.bits, ob) and np.array_equal(out3.iterations, oi) and np.array_equal(out3.synd_ok, ok)
+    # errors of any shard surface (no silent partial results)
+    with pytest.raises(Q.QLDPCError):
+        g3.decode(Q.Params(Q.SPA, 0, True, 100.0), llr, s)
+
+
+@pytest.mark.gpu
+def test_simulation_statistics_independent_of_sharding(gpu_available, tmp_path):
+    """simulation.run over 3 logical shards on device 0 gives the same
+    per-combination statistics as one shard (uneven slices of 40 trials)."""
+    import json
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from qkd_ldpc_v_amd import simulation as S
+    from test_simulation import cfg_path, mtrx_dir
+
+    c = json.load(open(cfg_path("legacy_1k")))
+    c["trials_number"] = 40
+    c["code_rate_QBER_maps"] = [{"code_rate": 0.9, "QBER_begin": 0.02, "QBER_end": 0.03, "QBER_step": 0.01}]
+    cp = tmp_path / "c1.json"
+    cp.write_text(json.dumps(c))
+    cfg = S.Config.load(str(cp))
+    d = mtrx_dir(tmp_path, "c1_n1024_m220.alist")
+    mats, combos = S.prepare(cfg, S.matrix_files(d))
+    r1 = S.run(cfg, mats, combos, log=lambda *a: None)
+    r3 = S.run(cfg, mats, combos, log=lambda *a: None, devices=[0, 0, 0])
+    drop = ("tp_mean", "tp_std", "tp_min", "tp_max")
+    strip = lambda rs: [{k: v for k, v in r.items() if k not in drop} for r in rs]  # noqa: E731
+    assert strip(r1) == strip(r3)

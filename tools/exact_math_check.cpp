@@ -22,8 +22,11 @@ static inline uint64_t sm64(uint64_t &s) {
 static inline double u01(uint64_t &s) { return (sm64(s) >> 11) * 0x1.0p-53; }
 static thread_local int dummy_flag = 0;
 // the decoder's expm1 class table (exact_math.h: tanh_half_common_t)
-static ql_exact::Expm1Class g_ctab[ql_exact::EXPM1_CLASSES];
-static double tanh_t(double b, double lim, double tl) { return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, g_ctab); }
+static ql_exact::Expm1A g_ctab_a[ql_exact::EXPM1_CLASSES];
+static ql_exact::Expm1B g_ctab_b[ql_exact::EXPM1_CLASSES];
+static double tanh_t(double b, double lim, double tl) {
+    return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_b});
+}
 static inline bool same(double a, double b) {
     if (a != a && b != b) return true;
     uint64_t x, y; memcpy(&x, &a, 8); memcpy(&y, &b, 8); return x == y;
@@ -43,7 +46,8 @@ int main(int argc, char **argv) {
     long per = argc > 1 ? atol(argv[1]) : 1000000;
     uint64_t seed0 = argc > 2 ? strtoull(argv[2], 0, 10) : 12345;
     unsigned nt = std::thread::hardware_concurrency(); if (!nt) nt = 4;
-    for (int i = 0; i < ql_exact::EXPM1_CLASSES; ++i) g_ctab[i] = ql_exact::expm1_class(i + ql_exact::EXPM1_K_MIN);
+    for (int i = 0; i < ql_exact::EXPM1_CLASSES; ++i)
+        ql_exact::expm1_class(i + ql_exact::EXPM1_K_MIN, &g_ctab_a[i], &g_ctab_b[i]);
     const char *names[15] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec", "tanh_half_dec", "atanh2_dec", "tanh_half_clip", "atanh2_clip", "tanh_half_clip_t"};
     std::atomic<long> bad[15]; for (auto &b : bad) b = 0;
     std::vector<std::thread> th;
