@@ -67,6 +67,10 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     // frame claim order (order.hip): per-frame weights and the sorted order
     int32_t *fweight = nullptr, *forder = nullptr;
     size_t order_frames = 0;
+    // relabelled graphs, frames from llr[] (palettize): the llr of frames the
+    // palette cannot hold, in label order (batch x n; allocated on first need)
+    double *llr_lab = nullptr;
+    size_t llr_lab_frames = 0;
     // kernel timing (qldpc_set_kernel_timing): events around the last decode launch
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
@@ -1112,8 +1116,26 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         if (a.rows_wg_offset >= 0 && !a.vn_rows)
             return fail(QLDPC_EUNSUP, "this code's min-sum row aggregates need the bit gather (QLDPC_VNG=0 given)");
     }
-    if (v2 && !codes_ready)
-        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, dg->col_orig, stream));
+    if (v2 && !codes_ready) {
+        // relabelled graphs read a non-paletted frame's llr[] by label: palettize
+        // writes those frames' LLRs in label order into the workspace
+        double *llr_lab = nullptr;
+        if (dg->col_orig) {
+            std::lock_guard<std::mutex> lk(dg->mu);
+            if ((size_t)batch > w->llr_lab_frames) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                (void)hipFree(w->llr_lab);
+                w->llr_lab = nullptr;
+                w->llr_lab_frames = 0;
+                HIP_TRY(hipMalloc(&w->llr_lab, (size_t)batch * g->n * sizeof(double)));
+                w->llr_lab_frames = (size_t)batch;
+            }
+            llr_lab = w->llr_lab;
+            a.llr = llr_lab;
+        }
+        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, dg->col_orig, llr_lab,
+                                 stream));
+    }
     {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order).
         // It only schedules — results never depend on it — so a shape it cannot
         // run (LDS beyond the device limit) decodes in index order instead.
@@ -1313,6 +1335,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(kv.second.palette);
             (void)hipFree(kv.second.pal_ok);
             (void)hipFree(kv.second.split_ctl);
+            (void)hipFree(kv.second.llr_lab);
             if (kv.second.ev0) (void)hipEventDestroy(kv.second.ev0);
             if (kv.second.ev1) (void)hipEventDestroy(kv.second.ev1);
             (void)hipFree(kv.second.gtotal);

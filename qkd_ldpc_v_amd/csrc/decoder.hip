@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(256) math_selftest_kernel(int fn, int count, c
     __shared__ ql_exact::Expm1B ctab_b[ql_exact::EXPM1_CLASSES];
     if (threadIdx.x < ql_exact::EXPM1_CLASSES)
         ql_exact::expm1_class(threadIdx.x + ql_exact::EXPM1_K_MIN, &ctab_a[threadIdx.x], &ctab_b[threadIdx.x]);
-    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b};
+    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b, 1};
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;

@@ -138,8 +138,8 @@ struct DecodeArgs {
     // Bank-aware bit labels (relabel.cpp; one-workgroup register shapes): the
     // graph's metadata and the frame codes use labels, llr / bits / posterior
     // the reference's bit ids.  nullptr: identity.
-    const int32_t *col_orig;        // [n] label -> bit id
-    const int32_t *col_lab;         // [n] bit id -> label
+    const int32_t *col_orig;        // [n] label -> bit id (the frame codes and llr[] the kernel reads are in labels)
+    const int32_t *col_lab;         // [n] bit id -> label (outputs: bits / posterior in bit ids)
 };
 
 // The persistent decoders' frame claim: the next frame of the launch's claim
@@ -175,7 +175,7 @@ constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per la
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
+                            uint8_t *pal_ok, const int32_t *col_orig, double *llr_lab, hipStream_t stream);
 size_t trials_lds_bytes(int n);
 size_t trials_scratch_words(int n, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,

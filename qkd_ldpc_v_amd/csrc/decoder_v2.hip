@@ -238,12 +238,13 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // SPA: the expm1 class table of tanh_half_clip_t, once per workgroup (the
     // frame loop's first barrier orders it before any scan)
     // (two arrays of 16-byte entries: A at L.ctab, B right after A)
+    // (entries of 32 bytes: A = {X3, X4} then B = {B, C, k << 20}; see exact_math.h)
     ql_exact::Expm1A *const ctab_a = reinterpret_cast<ql_exact::Expm1A *>(smem + L.ctab);
-    ql_exact::Expm1B *const ctab_b = reinterpret_cast<ql_exact::Expm1B *>(smem + L.ctab) + ql_exact::EXPM1_CLASSES;
-    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b};
+    ql_exact::Expm1B *const ctab_b = reinterpret_cast<ql_exact::Expm1B *>(smem + L.ctab) + 1;
+    const ql_exact::Expm1Tab ctab{ctab_a, ctab_b, 2};
     if constexpr (ALG == 0) {
         if (tid < ql_exact::EXPM1_CLASSES)
-            ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN, &ctab_a[tid], &ctab_b[tid]);
+            ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN, &ctab_a[2 * tid], &ctab_b[2 * tid]);
     }
 #ifdef QL_PHASE_STAMPS
     uint64_t st_acc[NUM_STAMPS];
@@ -384,9 +385,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 if (paletted) return pal[codes[col]];
             }
-            // (llr[] is in the reference's bit order: map a label back)
-            const int cg = a.col_orig ? a.col_orig[col] : col;
-            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, cg * 8, 0, 0));
+            // (relabelled graphs: decode_on hands over llr[] in label order)
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
         };
         // total starts as the channel LLRs: the check-node scan of iteration 0
         // reads the channel decision from it, and bits of degree 0 keep it.
@@ -1136,7 +1136,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 // with more gets pal_ok = 0 and the decoder gathers its llr[] instead.  Unused
 // entries repeat entry 0 (the SPA iteration-0 test reads all four).
 __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const double *llr, uint8_t *codes,
-                                                        double *palette, uint8_t *pal_ok, const int32_t *col_orig) {
+                                                        double *palette, uint8_t *pal_ok, const int32_t *col_orig,
+                                                        double *llr_lab) {
     __shared__ unsigned long long pv[4];
     __shared__ int pcount, over;
     const size_t f = blockIdx.x;
@@ -1180,6 +1181,8 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
                 const unsigned long long x = v[col_orig ? col_orig[i] : i];
                 for (int q = 1; q < 4; ++q)
                     if (q < cnt && x == pv[q]) code = q;
+                // a frame the palette cannot hold is decoded from llr[]: in label order
+                if (llr_lab && over) llr_lab[f * (size_t)n + i] = __builtin_bit_cast(double, x);
             }
             byte |= code << (2 * s);
         }
@@ -1280,10 +1283,10 @@ hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_b
 }
 
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream) {
+                            uint8_t *pal_ok, const int32_t *col_orig, double *llr_lab, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(palettize_kernel, dim3(batch), dim3(256), 0, stream, n, nc, llr, codes, palette, pal_ok,
-                       col_orig);
+                       col_orig, llr_lab);
     return hipGetLastError();
 }
 

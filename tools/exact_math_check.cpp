@@ -25,7 +25,7 @@ static thread_local int dummy_flag = 0;
 static ql_exact::Expm1A g_ctab_a[ql_exact::EXPM1_CLASSES];
 static ql_exact::Expm1B g_ctab_b[ql_exact::EXPM1_CLASSES];
 static double tanh_t(double b, double lim, double tl) {
-    return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_b});
+    return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_b, 1});
 }
 static inline bool same(double a, double b) {
     if (a != a && b != b) return true;
