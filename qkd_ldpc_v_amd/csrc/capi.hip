@@ -163,7 +163,8 @@ struct qldpc_graph {
     int n = 0, m = 0, E = 0, T = 0, EPL = 0, dv_max = 0, max_dc = 0, variant = 0;
     bool vng = false;                       // V2 min-sum bit gather tables built
     bool vng_h_fit = false;                 // hybrid bit gather's padded edge codes fit LDS (set before planning)
-    bool rows_global_ms = false;            // hybrid min-sum: row aggregates in global scratch
+    bool rows_global_ms = false;            // hybrid min-sum: row aggregates (partly) in global scratch
+    int rows_lds_ms = 0, rows_lds_waves_ms = 0;  // ... of which the rows of the first waves stay in LDS
     int v2R = 0, v2RG = 0, n_iso = 0;       // V2: register / scratch slots per lane, bits of degree 0
     std::vector<int> wave_rows;             // V2: first layout row of each wave (+ m)
     std::vector<int> row_order;             // V2: layout row -> original row
@@ -198,7 +199,8 @@ int block_threads(const qldpc_graph &g) {
 
 size_t lds_of(const qldpc_graph &g, int alg) {
     if (g.variant == VAR_V2 && g.split_k > 1) return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true);
-    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG, g.rows_global_ms && alg >= 2)
+    return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG,
+                                              (g.rows_global_ms && alg >= 2) ? g.rows_lds_ms : -1)
                                : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
@@ -340,7 +342,7 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         if (lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1]) > LDS_LIMIT) {
             if (sh[1] == 0 || !g.vng_h_fit || g.m >= 0xFFFF ||
                 lds_bytes_v2(0, g.n, g.m, W * 64, false, sh[0], sh[1]) > LDS_LIMIT ||
-                lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], true) > LDS_LIMIT)
+                lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], 0) > LDS_LIMIT)
                 continue;
             rows_global = true;
         }
@@ -375,6 +377,16 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         g.v2R = sh[0];
         g.v2RG = sh[1];
         g.rows_global_ms = rows_global;
+        g.rows_lds_ms = g.m;
+        g.rows_lds_waves_ms = W;
+        if (rows_global) {
+            // keep the rows of as many leading waves in LDS as fit beside the
+            // totals (QLDPC_ROWS_LDS=0: none, A/B)
+            int wl = env_int("QLDPC_ROWS_LDS", 1) ? W : 0;
+            while (wl > 0 && lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], rb[wl]) > LDS_LIMIT) --wl;
+            g.rows_lds_waves_ms = wl;
+            g.rows_lds_ms = rb[wl];
+        }
         g.T = W * 64;
         g.EPL = epl;
         g.wave_rows = rb;
@@ -836,8 +848,10 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         for (int w = 0; w < W; ++w) full += (long long)(g->dv_max - 1) * lepl[w * 64];
         fprintf(stderr, "{\"plan\": {\"waves\": %d, \"slots_reg\": %d, \"slots_scratch\": %d, \"epl_max\": %d, "
                         "\"dv_max\": %d, \"vn_slot_visits_csr\": %lld, \"vn_slot_visits_kpos_sorted\": %lld, "
-                        "\"vn_slot_visits_unmasked\": %lld}}\n",
-                W, g->v2R, g->v2RG, g->EPL, g->dv_max, visited(vnm), visited(vnm_ms), full);
+                        "\"vn_slot_visits_unmasked\": %lld, \"rows_global_ms\": %d, \"rows_lds_ms\": %d, "
+                        "\"rows_lds_waves_ms\": %d}}\n",
+                W, g->v2R, g->v2RG, g->EPL, g->dv_max, visited(vnm), visited(vnm_ms), full, (int)g->rows_global_ms,
+                g->rows_lds_ms, g->rows_lds_waves_ms);
         fprintf(stderr, "{\"relabel\": {\"excess_before\": %lld, \"excess_after\": %lld, \"cycles_before\": %lld, "
                         "\"cycles_after\": %lld}}\n",
                 g->relabel_stats[0], g->relabel_stats[1], g->relabel_stats[2], g->relabel_stats[3]);
@@ -1076,6 +1090,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
     a.stage_wg_offset = (long long)g->v2RG * REG_TSTRIDE;
     a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
+    a.rows_lds = (v2 && g->rows_global_ms && alg >= 2) ? g->rows_lds_ms : g->m;
+    a.rows_lds_waves = (v2 && g->rows_global_ms && alg >= 2) ? g->rows_lds_waves_ms : (g->T / 64);
     a.row_orig = dg->row_orig;
     a.col_orig = dg->col_orig;
     a.col_lab = dg->col_lab;

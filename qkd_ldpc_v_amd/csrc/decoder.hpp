@@ -135,6 +135,8 @@ struct DecodeArgs {
     // (C5 R=0.5: m = 5120): rowAB lives in the workgroup's global scratch
     // (L2-resident) at this offset in doubles; -1: rows in LDS.
     long long rows_wg_offset;
+    int rows_lds;                   // ... of which the leading rows_lds layout rows stay in LDS (m: all)
+    int rows_lds_waves;             // = the rows of waves 0 .. rows_lds_waves - 1
     // Bank-aware bit labels (relabel.cpp; one-workgroup register shapes): the
     // graph's metadata and the frame codes use labels, llr / bits / posterior
     // the reference's bit ids.  nullptr: identity.
@@ -165,8 +167,8 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                const int32_t *col_orig, hipStream_t stream);
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0,
-                    bool rows_global = false);
+// rows_lds: min-sum row aggregates kept in LDS on the hybrid shape (-1: all m).
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0, int rows_lds = -1);
 // Whether a V2 shape can run the min-sum bit gather (DecodeArgs::vn_rows):
 // the dv <= 4 register shape, or the hybrid shape when the padded edge
 // positions' two code bits fit the LDS byte area.

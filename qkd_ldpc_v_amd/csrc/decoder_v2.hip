@@ -101,7 +101,7 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL);
-    else return V2Layout(a.n, RGLB ? 0 : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
+    else return V2Layout(a.n, RGLB ? a.rows_lds : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
 // Whether a launch runs the LDS-slot instantiation (RL = V2_RL): SPA family,
@@ -193,8 +193,31 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     double2 *const rowAB_lds = reinterpret_cast<double2 *>(smem + L.rows); // min-sum
     double *rowA = rowA_lds;
     double2 *rowAB = rowAB_lds;
-    if constexpr (RGLB)
-        rowAB = reinterpret_cast<double2 *>(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.rows_wg_offset);
+    // RGLB: the leading a.rows_lds layout rows (the rows of waves
+    // 0 .. a.rows_lds_waves - 1) stay in LDS, the others live in the
+    // workgroup's global scratch.  A wave's scan and message pass touch only
+    // its own rows, so there the choice is one scalar branch per access.
+    double2 *const rowAB_glb =
+        RGLB ? reinterpret_cast<double2 *>(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.rows_wg_offset)
+             : nullptr;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool rows_in_lds = !RGLB || wave < a.rows_lds_waves;
+    auto row_ld = [&](int r) -> double2 {
+        if constexpr (RGLB) {
+            if (rows_in_lds) return rowAB_lds[r];
+            return rowAB_glb[r];
+        } else {
+            return rowAB[r];
+        }
+    };
+    auto row_st = [&](int r, double2 v) {
+        if constexpr (RGLB) {
+            if (rows_in_lds) rowAB_lds[r] = v;
+            else rowAB_glb[r] = v;
+        } else {
+            rowAB[r] = v;
+        }
+    };
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
     uint8_t *codes = smem + V2_CODES_OFF;
 
@@ -205,7 +228,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     meta.init(a.slot_meta, tid, T);
     // VN phase kk visits only the slots where some lane of this wave holds the
     // kk-th edge of a bit (capi.hip: vn_mask[wave][kk]).
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t *vn_mask = a.vn_mask + (size_t)wave * a.dv_max;
     // ... and per slot, the lanes whose edge there is a bit's kk-th: an exec
     // mask loaded by the scalar unit (no per-lane kpos test).
@@ -581,7 +603,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                             double2 ab[4];
     #pragma unroll
                             for (int q = 0; q < 4; ++q)
-                                ab[q] = rowAB[(int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu)];
+                            {
+                                const int rq = (int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu);
+                                if constexpr (RGLB) ab[q] = (rq < a.rows_lds) ? rowAB_lds[rq] : rowAB_glb[rq];
+                                else ab[q] = rowAB[rq];
+                            }
     #pragma unroll
                             for (int q = 0; q < 4; ++q) {
                                 const double c = ms_message(ab[q], (cb >> (2 * q)) & 1u, ((cb >> (2 * q)) & 2u) != 0, DC);
@@ -952,7 +978,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // the first START closes the tail segment: park its aggregate
                         // (parity of negatives in min1's sign bit) in the split row's
                         // own entry, which nothing else touches until the merge below
-                        if (k == head) rowAB[row0] = ms_pack(m1, m2, neg, 0);
+                        if (k == head) row_st(row0, ms_pack(m1, m2, neg, 0));
                     }
                     m1 = start ? DBL_MAX : m1;
                     m2 = start ? DBL_MAX : m2;
@@ -972,7 +998,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         rowA[r] = acc;
                         if constexpr (ALG == 0) div_unsafe |= (__builtin_fabs(acc) >= 0x1p-900) ? 0 : 1;
                     } else {
-                        rowAB[r] = ms_pack(m1, m2, cur_s ^ neg, mr);
+                        row_st(r, ms_pack(m1, m2, cur_s ^ neg, mr));
                         big |= (m2 > thr) ? 1 : 0;
                     }
                 }
@@ -1003,14 +1029,14 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     t.m2 = __shfl(m2, up, 64);
                     t.neg = __shfl(neg, up, 64);
                     if (head > 0) {
-                        const double2 ta = rowAB[row0];
+                        const double2 ta = row_ld(row0);
                         MinAgg h;
                         h.m1 = __builtin_fabs(ta.x);
                         h.m2 = ta.y;
                         h.neg = (int)(ql_exact::hi_word(ta.x) >> 31);
                         agg_merge(t, h);
                         const int mr = ppar ^ hpar ^ s_row0;
-                        rowAB[row0] = ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr);
+                        row_st(row0, ms_pack(t.m1, t.m2, s_row0 ^ t.neg, mr));
                         big |= (t.m2 > thr) ? 1 : 0;
                         mis |= mr;
                     }
@@ -1069,7 +1095,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 } else {
                     const double x = c2b.get(k);
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
-                    const double2 ab = rowAB[r];
+                    const double2 ab = row_ld(r);
                     const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
                     c = ms_message(ab, xneg, eq1, msclip);
                     if constexpr (VNG_H) {
@@ -1244,10 +1270,10 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, bool rows_global) {
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds) {
     if (split) return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m) ? V2_RL_SPLIT : 0).bytes;
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
-    return V2Layout(n, rows_global ? 0 : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
+    return V2Layout(n, rows_lds >= 0 ? rows_lds : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
                     V2_ROWSCAN_ON && !split && RG == 0).bytes;
 }
 

@@ -9,6 +9,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out/round_prof
+if [ "${CLEAN:-0}" = 1 ]; then rm -rf "$OUT"; fi  # (a round's first call: no passes of an older build mix in)
 mkdir -p "$OUT"
 pass() {  # name, bench args, rocprof args...
   local name=$1; local bargs=$2; shift 2
