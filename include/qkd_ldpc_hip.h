@@ -186,6 +186,15 @@ int qldpc_graph_labels(const qldpc_graph *g, int32_t *labels_out, int64_t *stats
 int qldpc_set_kernel_timing(qldpc_graph *g, int32_t enabled);
 int qldpc_last_decode_kernel_ms(qldpc_graph *g, int32_t device, void *stream, float *ms);
 
+/* Diagnostic: the order in which the last decode on (device, stream) claimed
+ * its frames (order.hip: ascending weight |H * z XOR s| of the channel
+ * decision z) and each frame's weight, indexed by frame.  *count = the batch,
+ * or 0 when that decode claimed frames in index order (QLDPC_ORDER=0, one
+ * frame).  Waits for the stream.  No counterpart in the reference (its pool
+ * decodes trials one at a time). */
+int qldpc_last_claim_order(qldpc_graph *g, int32_t device, void *stream, int32_t *order_out, int32_t *weight_out,
+                           int32_t cap, int32_t *count);
+
 /* Diagnostic: evaluate the decoder's device math on `count` inputs on the
  * current device — fn 0 tanh, 1 atanh, 2 expm1, 3 log1p (exact_math.h, the
  * glibc-exact restatement), 4 tanh_lin_approx, 5 atanh_lin_approx

@@ -65,6 +65,7 @@ _SIGNATURES = {
     "qldpc_graph_destroy": (None, [_P]),
     "qldpc_set_kernel_timing": (_I32, [_P, _I32]),
     "qldpc_last_decode_kernel_ms": (_I32, [_P, _I32, _P, ctypes.POINTER(ctypes.c_float)]),
+    "qldpc_last_claim_order": (_I32, [_P, _I32, _P, _P, _P, _I32, _PI32]),
     "qldpc_graph_info": (_I32, [_P, _PI32, _PI32, _PI32, _PI32]),
     "qldpc_graph_plan": (_I32, [_P, _I32, _I32, _PI32, _PI32, _PI32, _PI32, ctypes.POINTER(ctypes.c_char_p)]),
     "qldpc_decode_batch": (_I32, [_P, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P, _P, _P, _P]),

@@ -67,6 +67,7 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     // frame claim order (order.hip): per-frame weights and the sorted order
     int32_t *fweight = nullptr, *forder = nullptr;
     size_t order_frames = 0;
+    int order_count = 0;  // frames of the last decode claimed through forder (0: index order)
     // relabelled graphs, frames from llr[] (palettize): the llr of frames the
     // palette cannot hold, in label order (batch x n; allocated on first need)
     double *llr_lab = nullptr;
@@ -1165,6 +1166,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
             if (oe == hipSuccess) a.frame_order = w->forder;
             else (void)hipGetLastError();  // clear the sticky launch error; index order
         }
+        w->order_count = a.frame_order ? batch : 0;
     }
     HIP_TRY(hipMemsetAsync(w->counter, 0, sizeof(int), stream));
 #ifdef QL_PHASE_STAMPS
@@ -1427,6 +1429,35 @@ int qldpc_last_decode_kernel_ms(qldpc_graph *g, int32_t device, void *stream, fl
     if (e == hipSuccess) e = hipEventElapsedTime(ms, e0, e1);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) return hip_fail(e, "decode kernel events");
+    return QLDPC_OK;
+}
+
+int qldpc_last_claim_order(qldpc_graph *g, int32_t device, void *stream, int32_t *order_out, int32_t *weight_out,
+                           int32_t cap, int32_t *count) {
+    if (!g || !count) return fail(QLDPC_EINVAL, "graph / count is NULL");
+    DeviceGraph *dg = find_dev(g, device);
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    int32_t *ord = nullptr, *wt = nullptr;
+    int cnt = 0;
+    {
+        std::lock_guard<std::mutex> lk(dg->mu);
+        auto it = dg->ws.find(stream);
+        if (it == dg->ws.end()) return fail(QLDPC_EINVAL, "no decode on that stream");
+        ord = it->second.forder;
+        wt = it->second.fweight;
+        cnt = it->second.order_count;
+    }
+    *count = cnt;
+    if (cnt == 0) return QLDPC_OK;
+    if (cap < cnt) return fail(QLDPC_EINVAL, "order buffer smaller than the last batch");
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    HIP_TRY(hipSetDevice(device));
+    hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    if (e == hipSuccess && order_out) e = hipMemcpy(order_out, ord, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && weight_out) e = hipMemcpy(weight_out, wt, (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToHost);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) return hip_fail(e, "claim order copy");
     return QLDPC_OK;
 }
 

@@ -63,7 +63,8 @@ class HMatrix:
         b = np.asarray(bits, np.uint8)
         vals = b[..., self.col_idx].astype(np.int64)
         cs = np.concatenate([np.zeros(b.shape[:-1] + (1,), np.int64), np.cumsum(vals, axis=-1)], axis=-1)
-        return ((cs[..., self.row_ptr[1:]] - cs[..., self.row_ptr[:-1]]) & 1).astype(np.uint8)
+        # (advanced indexing on the last axis yields a Fortran-ordered result: make it row-major)
+        return np.ascontiguousarray(((cs[..., self.row_ptr[1:]] - cs[..., self.row_ptr[:-1]]) & 1).astype(np.uint8))
 
 
 def load_matrix(path: str, fmt: int) -> HMatrix:
@@ -164,6 +165,18 @@ class Graph:
               "qldpc_last_decode_kernel_ms")
         return float(ms.value)
 
+    def last_claim_order(self, stream=None, device: int = 0, cap: int = 1 << 20):
+        """(order, weight) of the last decode on (device, stream): the claim
+        order and each frame's weight, or (None, None) for index order."""
+        order = np.empty(cap, np.int32)
+        weight = np.empty(cap, np.int32)
+        cnt = ctypes.c_int32(0)
+        check(lib().qldpc_last_claim_order(self._g, device, _stream_ptr(stream, device), order.ctypes.data,
+                                           weight.ctypes.data, cap, ctypes.byref(cnt)), "qldpc_last_claim_order")
+        if cnt.value == 0:
+            return None, None
+        return order[:cnt.value].copy(), weight[:cnt.value].copy()
+
     # ---- host-buffer decode (synchronous, shards over the graph's devices) ----
     def decode(self, params: Params, llr: np.ndarray, syndrome: np.ndarray, posterior: bool = False) -> DecodeOutput:
         llr = np.ascontiguousarray(llr, np.float64)
@@ -190,14 +203,14 @@ class Graph:
         dev = llr.device.index if device is None else device
         p = params.c()
         check(lib().qldpc_decode_batch_device(
-            self._g, dev, ctypes.byref(p), int(llr.shape[0]), llr.data_ptr(), syndrome.data_ptr(), bits.data_ptr(),
-            iters.data_ptr(), ok.data_ptr(), None if posterior is None else posterior.data_ptr(),
+            self._g, dev, ctypes.byref(p), int(llr.shape[0]), _dp(llr), _dp(syndrome), _dp(bits),
+            _dp(iters), _dp(ok), _dp(posterior),
             _stream_ptr(stream, dev)), "qldpc_decode_batch_device")
 
     def build_frames_device(self, alice, bob, log_p, llr, syndrome, stream=None, device: int | None = None) -> None:
         dev = alice.device.index if device is None else device
-        check(lib().qldpc_build_frames_device(self._g, dev, int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(),
-                                              log_p.data_ptr(), llr.data_ptr(), syndrome.data_ptr(),
+        check(lib().qldpc_build_frames_device(self._g, dev, int(alice.shape[0]), _dp(alice), _dp(bob),
+                                              _dp(log_p), _dp(llr), _dp(syndrome),
                                               _stream_ptr(stream, dev)), "qldpc_build_frames_device")
 
     def qkd_ldpc_device(self, params: Params, alice, bob, log_p, llr_ws, synd_ws, bits, iters, ok, keys_match,
@@ -206,9 +219,9 @@ class Graph:
         dev = alice.device.index if device is None else device
         p = params.c()
         check(lib().qldpc_qkd_ldpc_batch_device(
-            self._g, dev, ctypes.byref(p), int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(), log_p.data_ptr(),
-            llr_ws.data_ptr(), synd_ws.data_ptr(), bits.data_ptr(), iters.data_ptr(), ok.data_ptr(),
-            keys_match.data_ptr(), _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_batch_device")
+            self._g, dev, ctypes.byref(p), int(alice.shape[0]), _dp(alice), _dp(bob), _dp(log_p),
+            _dp(llr_ws), _dp(synd_ws), _dp(bits), _dp(iters), _dp(ok),
+            _dp(keys_match), _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_batch_device")
 
 
     def rate_plan(self, punctured, shortened) -> "RatePlan":
@@ -221,17 +234,17 @@ class Graph:
         dev = alice.device.index if device is None else device
         p = params.c()
         check(lib().qldpc_qkd_ldpc_rate_adapt_batch_device(
-            self._g, plan.handle, dev, ctypes.byref(p), int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(),
-            punct_alice.data_ptr(), punct_bob.data_ptr(), log_p.data_ptr(), alice_ext.data_ptr(), llr_ws.data_ptr(),
-            synd_ws.data_ptr(), bits.data_ptr(), iters.data_ptr(), ok.data_ptr(), keys_match.data_ptr(),
+            self._g, plan.handle, dev, ctypes.byref(p), int(alice.shape[0]), _dp(alice), _dp(bob),
+            _dp(punct_alice), _dp(punct_bob), _dp(log_p), _dp(alice_ext), _dp(llr_ws),
+            _dp(synd_ws), _dp(bits), _dp(iters), _dp(ok), _dp(keys_match),
             _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_rate_adapt_batch_device")
 
     def build_frames_rate_adapt_device(self, plan: "RatePlan", alice, bob, punct_alice, punct_bob, log_p, alice_ext,
                                        llr, syndrome, stream=None, device: int | None = None) -> None:
         dev = alice.device.index if device is None else device
         check(lib().qldpc_build_frames_rate_adapt_device(
-            self._g, plan.handle, dev, int(alice.shape[0]), alice.data_ptr(), bob.data_ptr(), punct_alice.data_ptr(),
-            punct_bob.data_ptr(), log_p.data_ptr(), alice_ext.data_ptr(), llr.data_ptr(), syndrome.data_ptr(),
+            self._g, plan.handle, dev, int(alice.shape[0]), _dp(alice), _dp(bob), _dp(punct_alice),
+            _dp(punct_bob), _dp(log_p), _dp(alice_ext), _dp(llr), _dp(syndrome),
             _stream_ptr(stream, dev)), "qldpc_build_frames_rate_adapt_device")
 
 
@@ -256,8 +269,8 @@ class RatePlan:
 
 def keys_match_device(alice, bits, out, stream=None) -> None:
     dev = alice.device.index
-    check(lib().qldpc_keys_match_device(int(alice.shape[0]), int(alice.shape[1]), alice.data_ptr(), bits.data_ptr(),
-                                        out.data_ptr(), _stream_ptr(stream, dev)), "qldpc_keys_match_device")
+    check(lib().qldpc_keys_match_device(int(alice.shape[0]), int(alice.shape[1]), _dp(alice), _dp(bits),
+                                        _dp(out), _stream_ptr(stream, dev)), "qldpc_keys_match_device")
 
 
 def trial_seeds(simulation_seed: int, count: int) -> np.ndarray:
@@ -276,8 +289,8 @@ def trials_device(n: int, qber: float, seeds, alice, bob, seed_add: int = 0, str
 
     dev = seeds.device.index
     q = ctypes.c_double(0.0)
-    check(lib().qldpc_trials_device(int(n), float(qber), int(seeds.shape[0]), seeds.data_ptr(),
-                                    int(seed_add) & 0xFFFFFFFFFFFFFFFF, alice.data_ptr(), bob.data_ptr(),
+    check(lib().qldpc_trials_device(int(n), float(qber), int(seeds.shape[0]), _dp(seeds),
+                                    int(seed_add) & 0xFFFFFFFFFFFFFFFF, _dp(alice), _dp(bob),
                                     ctypes.byref(q), _stream_ptr(stream, dev)), "qldpc_trials_device")
     return q.value
 
@@ -316,12 +329,23 @@ def trials_rate_adapt_device(n: int, qber: float, seeds, n_punct: int, alice, bo
 
     dev = seeds.device.index
     q = ctypes.c_double(0.0)
-    check(lib().qldpc_trials_rate_adapt_device(int(n), float(qber), int(seeds.shape[0]), seeds.data_ptr(),
-                                               int(seed_add) & 0xFFFFFFFFFFFFFFFF, int(n_punct), alice.data_ptr(),
-                                               bob.data_ptr(), punct_alice.data_ptr(), punct_bob.data_ptr(),
+    check(lib().qldpc_trials_rate_adapt_device(int(n), float(qber), int(seeds.shape[0]), _dp(seeds),
+                                               int(seed_add) & 0xFFFFFFFFFFFFFFFF, int(n_punct), _dp(alice),
+                                               _dp(bob), _dp(punct_alice), _dp(punct_bob),
                                                ctypes.byref(q), _stream_ptr(stream, dev)),
           "qldpc_trials_rate_adapt_device")
     return q.value
+
+
+def _dp(t):
+    """Device pointer of a row-major (C-contiguous) tensor: the C ABI reads
+    frames as [frame][bit] rows, so a transposed view would be misread."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError(f"device buffers must be C-contiguous (row-major); got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    return t.data_ptr()
 
 
 def _stream_ptr(stream, device: int):

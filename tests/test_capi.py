@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, load_fixture
 import qkd_ldpc_v_amd as Q
 from qkd_ldpc_v_amd import HMatrix, QLDPCError
 
@@ -97,3 +97,20 @@ def test_relabelling_only_on_one_workgroup_register_shapes():
             os.environ.pop("QLDPC_RELABEL")
         else:
             os.environ["QLDPC_RELABEL"] = old
+
+
+def test_device_entries_refuse_non_row_major_buffers():
+    """The C ABI reads [frame][bit] rows: a transposed (column-major) tensor is
+    refused before any call, and the host syndrome helper is row-major (numpy's
+    last-axis fancy indexing returns Fortran order, which torch.from_numpy keeps)."""
+    import torch
+
+    from qkd_ldpc_v_amd.graph import _dp
+
+    t = torch.zeros((4, 3), dtype=torch.uint8)
+    assert _dp(t) == t.data_ptr() and _dp(None) is None
+    with pytest.raises(ValueError, match="C-contiguous"):
+        _dp(t.t())
+    H = load_fixture("c1_n1024_m220.alist")
+    a, _, _ = Q.bsc_frames(H.n, 0.03, 4, seed=1)
+    assert H.syndrome(a).flags["C_CONTIGUOUS"]

@@ -535,3 +535,48 @@ def test_host_threads_share_one_graph(gpu_available, name, alg, prim, sec):
     for x in th:
         x.join()
     assert not errors, f"{len(errors)} frames/calls differ; first {errors[:3]}"
+
+
+@pytest.mark.parametrize("name,alg,prim,sec,qber", [("c2_n10240_m2201.alist", Q.SPA, 0.0, 0.0, 0.0215),
+                                                     ("c3_n10240_m1801.alist", Q.OMSA, 0.77, 0.0, 0.016)])
+def test_frame_claim_order(gpu_available, monkeypatch, name, alg, prim, sec, qber):
+    """The claim order (order.hip) is a permutation of the batch in ascending
+    weight |H * z XOR s| of the channel decision z = (llr <= 0) — paletted and
+    soft-LLR frames alike, on relabelled graphs — and decoding in index order
+    (QLDPC_ORDER=0) gives identical results."""
+    import torch
+
+    H = load_fixture(name)
+    g = graph(name)
+    batch = 300
+    _, _, llr, s = frames(H, qber, batch, 17)
+    rng = np.random.default_rng(3)
+    llr[::7] *= rng.uniform(0.5, 2.0, size=llr[::7].shape)  # soft LLRs: beyond the 4-value palette
+    dev = torch.device("cuda:0")
+    p = Q.Params(alg, 50, True, 100.0, prim, sec)
+
+    def run():
+        tl, ts = torch.from_numpy(llr).to(dev), torch.from_numpy(s).to(dev)
+        bits = torch.empty((batch, H.n), dtype=torch.uint8, device=dev)
+        it = torch.empty(batch, dtype=torch.int32, device=dev)
+        ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+        post = torch.empty((batch, H.n), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        g.decode_device(p, tl, ts, bits, it, ok, post, stream=stream)
+        torch.cuda.synchronize()
+        order, weight = g.last_claim_order(stream)
+        return (bits.cpu().numpy(), it.cpu().numpy(), ok.cpu().numpy(), post.cpu().numpy()), order, weight
+
+    r1, order, weight = run()
+    assert order is not None and np.array_equal(np.sort(order), np.arange(batch))
+    w = (H.syndrome((llr <= 0).astype(np.uint8)) != s).sum(axis=1)
+    bad = np.nonzero(weight != w)[0]
+    assert bad.size == 0, (f"{bad.size} weights differ; frames {bad[:12].tolist()} gpu {weight[bad[:12]].tolist()} "
+                           f"host {w[bad[:12]].tolist()}; gpu weights {weight[:8].tolist()} host {w[:8].tolist()}")
+    assert np.all(np.diff(w[order]) >= 0)
+    monkeypatch.setenv("QLDPC_ORDER", "0")
+    r0, order0, _ = run()
+    assert order0 is None
+    for x, y in zip(r1[:3], r0[:3]):
+        assert np.array_equal(x, y)
+    assert bits_equal_nan(r1[3], r0[3])
