@@ -246,16 +246,21 @@ void plan(qldpc_graph &g) {
 // possible: contiguous blocks of rows first (consecutive check ids keep the
 // VN phase masks sparse), then swap / move single rows between the heaviest
 // and lightest waves.  Returns wave membership lists and the sums.
+// With weights wt, wave w's share of the edges is wt[w] / sum(wt) and its cap
+// cap * wt[w] (sums compared as sums[w] / wt[w]).
 std::vector<std::vector<int>> balance_rows(const int32_t *row_ptr, int m, int W, long long cap,
-                                           std::vector<long long> &sums) {
+                                           std::vector<long long> &sums, const std::vector<double> *wt = nullptr) {
     auto deg = [&](int j) { return row_ptr[j + 1] - row_ptr[j]; };
     const long long E = row_ptr[m];
+    std::vector<double> cw(W + 1, 0.0);  // cumulative weights
+    for (int w = 0; w < W; ++w) cw[w + 1] = cw[w] + (wt ? (*wt)[w] : 1.0);
+    auto wof = [&](int w) { return wt ? (*wt)[w] : 1.0; };
     std::vector<std::vector<int>> waves(W);
     sums.assign(W, 0);
     {
         int j = 0;
         for (int w = 0; w < W; ++w) {
-            const long long target = E * (w + 1) / W;
+            const long long target = wt ? (long long)std::llround((double)E * cw[w + 1] / cw[W]) : E * (w + 1) / W;
             while (j < m && (w == W - 1 || row_ptr[j + 1] <= target ||
                              (row_ptr[j] < target && target - row_ptr[j] > row_ptr[j + 1] - target))) {
                 waves[w].push_back(j);
@@ -269,10 +274,14 @@ std::vector<std::vector<int>> balance_rows(const int32_t *row_ptr, int m, int W,
     for (int w = 0; w < W; ++w)
         for (int j : waves[w]) by[w][deg(j)].push_back(j);
     for (int iter = 0; iter < 100000; ++iter) {
-        const int H = (int)(std::max_element(sums.begin(), sums.end()) - sums.begin());
-        const int L = (int)(std::min_element(sums.begin(), sums.end()) - sums.begin());
-        if (sums[H] <= cap || H == L) break;
-        const long long gap = sums[H] - sums[L];
+        int H = 0, L = 0;
+        for (int w = 1; w < W; ++w) {
+            if (sums[w] / wof(w) > sums[H] / wof(H)) H = w;
+            if (sums[w] / wof(w) < sums[L] / wof(L)) L = w;
+        }
+        if (sums[H] <= (long long)(cap * wof(H)) || H == L) break;
+        // (weighted: L's normalised load must stay below H's old one)
+        const long long gap = wt ? (long long)((double)sums[H] * wof(L) / wof(H)) - sums[L] : sums[H] - sums[L];
         // best transfer d (row of degree dx from H, optionally one of degree dy from L)
         long long best = 0;
         int bx = -1, by_ = -1;
@@ -349,30 +358,61 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         }
         const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
         std::vector<long long> sums;
-        const auto waves = balance_rows(row_ptr, g.m, W, cap, sums);
         std::vector<int> order, rb(W + 1, 0), nrp(g.m + 1, 0);
-        for (int w = 0; w < W; ++w) {
-            order.insert(order.end(), waves[w].begin(), waves[w].end());
-            rb[w + 1] = (int)order.size();
-        }
-        for (int j = 0; j < g.m; ++j) nrp[j + 1] = nrp[j] + (row_ptr[order[j] + 1] - row_ptr[order[j]]);
-        int epl = 0;
-        bool ok = true;
-        for (int w = 0; w < W && ok; ++w) {
-            const long long ew = nrp[rb[w + 1]] - nrp[rb[w]];
-            if (ew == 0) continue;
-            const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
-            ok = e <= R;
-            epl = std::max(epl, e);
-            // rows started per lane must fit the 32-bit syndrome mask
-            for (long long l = 0; l < 64 && ok; ++l) {
-                const long long e0 = nrp[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, nrp[rb[w + 1]]);
-                int starts = 0;
-                for (int j = rb[w]; j < rb[w + 1]; ++j)
-                    if (nrp[j] >= e0 && nrp[j] < e1) ++starts;
-                ok = starts <= 32;
+        int wl = W, epl = 0;
+        // Deal the rows with the waves past the first wl given `share` of a
+        // wave's edges; false when some lane would exceed the shape.
+        auto deal = [&](double share) -> bool {
+            std::vector<double> wt(W, 1.0);
+            wl = W;
+            for (int pass = 0; pass < 6; ++pass) {
+                const bool weighted = share != 1.0 && pass > 0;
+                const long long capw = weighted ? 64LL * std::max<long long>(
+                    (long long)std::ceil((double)E / (wl + (W - wl) * share) / 64.0), g.max_dc) : cap;
+                const auto waves = balance_rows(row_ptr, g.m, W, capw, sums, weighted ? &wt : nullptr);
+                order.clear();
+                for (int w = 0; w < W; ++w) {
+                    order.insert(order.end(), waves[w].begin(), waves[w].end());
+                    rb[w + 1] = (int)order.size();
+                }
+                for (int jr = 0; jr < g.m; ++jr)
+                    nrp[jr + 1] = nrp[jr] + (row_ptr[order[jr] + 1] - row_ptr[order[jr]]);
+                if (!rows_global) break;
+                int wn = env_int("QLDPC_ROWS_LDS", 1) ? W : 0;
+                while (wn > 0 && lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], rb[wn]) > LDS_LIMIT) --wn;
+                const bool agree = share == 1.0 || (pass > 0 && wn == wl);
+                wl = wn;
+                if (agree) break;
+                for (int w = 0; w < W; ++w) wt[w] = w < wl ? 1.0 : share;
             }
-        }
+            epl = 0;
+            for (int w = 0; w < W; ++w) {
+                const long long ew = nrp[rb[w + 1]] - nrp[rb[w]];
+                if (ew == 0) continue;
+                const int e = std::max<int>((int)((ew + 63) / 64), g.max_dc);
+                if (e > R) return false;
+                epl = std::max(epl, e);
+                // rows started per lane must fit the 32-bit syndrome mask
+                for (long long l = 0; l < 64; ++l) {
+                    const long long e0 = nrp[rb[w]] + l * e, e1 = std::min<long long>(e0 + e, nrp[rb[w + 1]]);
+                    int starts = 0;
+                    for (int jr = rb[w]; jr < rb[w + 1]; ++jr)
+                        if (nrp[jr] >= e0 && nrp[jr] < e1) ++starts;
+                    if (starts > 32) return false;
+                }
+            }
+            return true;
+        };
+        // Rows partly in global scratch: the waves whose rows stay in LDS are
+        // the leading wl (as many as fit), and the others read a row from L2
+        // per message.  Those get a smaller share of a wave's edges so the
+        // phase barriers do not wait on them (R=0.5 code: 65% is 4.5% faster
+        // than an even deal, tools/c5_share_ab.sh) — the smallest share from
+        // QLDPC_RGLB_SHARE (percent) up whose deal fits the shape.  wl
+        // depends on the deal, so each deal is redone until they agree.
+        bool ok = false;
+        const int share0 = rows_global ? std::min(100, std::max(10, env_int("QLDPC_RGLB_SHARE", 65))) : 100;
+        for (int sp = share0; sp <= 100 && !ok; sp += 5) ok = deal(sp / 100.0);
         if (!ok) continue;
         g.variant = VAR_V2;
         g.v2R = sh[0];
@@ -381,10 +421,8 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
         g.rows_lds_ms = g.m;
         g.rows_lds_waves_ms = W;
         if (rows_global) {
-            // keep the rows of as many leading waves in LDS as fit beside the
-            // totals (QLDPC_ROWS_LDS=0: none, A/B)
-            int wl = env_int("QLDPC_ROWS_LDS", 1) ? W : 0;
-            while (wl > 0 && lds_bytes_v2(2, g.n, g.m, W * 64, false, sh[0], sh[1], rb[wl]) > LDS_LIMIT) --wl;
+            // the rows of the leading wl waves stay in LDS beside the totals
+            // (QLDPC_ROWS_LDS=0: none, A/B)
             g.rows_lds_waves_ms = wl;
             g.rows_lds_ms = rb[wl];
         }

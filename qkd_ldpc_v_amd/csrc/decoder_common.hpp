@@ -134,6 +134,46 @@ struct EdgeMsgsH {
         if (k < R) return lp[(k - RV) * REG_TSTRIDE];
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (k - R) * REG_TSTRIDE * 8, 0));
     }
+    // For passes that visit every slot in order (the check-node scan, the
+    // message pass): the scratch slots of a group of four are requested
+    // together at the group's first slot, so their four L2 round trips overlap
+    // instead of each load waiting out the previous slot's store.
+    // (QL_SCRATCH_AHEAD: each group requested one group ahead — the first at
+    // the last register group's first slot)
+    double pre[4], nxt[4];
+    __device__ __forceinline__ double get_seq(int k) {
+        if constexpr (RG > 0) {
+            static_assert(R % 4 == 0 && RG % 4 == 0, "scratch slots come in groups of four");
+#ifdef QL_SCRATCH_AHEAD
+            if (k == R - 4) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) nxt[q] = get(R + q);
+            }
+            if (k >= R) {
+                const int j = k - R;
+                if ((j & 3) == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) pre[q] = nxt[q];
+                    if (j + 4 < RG) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) nxt[q] = get(k + 4 + q);
+                    }
+                }
+                return pre[j & 3];
+            }
+#else
+            if (k >= R) {
+                const int j = k - R;
+                if ((j & 3) == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) pre[q] = get(k + q);
+                }
+                return pre[j & 3];
+            }
+#endif
+        }
+        return get(k);
+    }
     __device__ __forceinline__ void set(int k, double x) {
         if (k < RV) {
             v[k] = x;

@@ -958,21 +958,21 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     // b2c = total - c2b (:115); c2b is +0 in iteration 0, so b = the
                     // channel LLR exactly there, and the clip (:122-123) is folded
                     // into tanh_half_clip with the iteration's (lim, thr).
-                    const double b = tv - c2b.get(k);
+                    const double b = tv - c2b.get_seq(k);
                     double t = b;
                     if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // tanh(b2c / 2.) (:60)
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
                 } else if constexpr (SPA_FAM) {
-                    const double x = clip_msg(tv - c2b.get(k), thr_it);  // (:115, :122-123; :21-29)
+                    const double x = clip_msg(tv - c2b.get_seq(k), thr_it);  // (:115, :122-123; :21-29)
                     double t = x;
                     if (compute) t = tanh_lin(x / 2.);
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;
                 } else {
-                    const double x = clip_msg(tv - c2b.get(k), thr_it);  // (:115, :122-123; :21-29)
+                    const double x = clip_msg(tv - c2b.get_seq(k), thr_it);  // (:115, :122-123; :21-29)
                     c2b.set(k, x);
                     if (k < KT && k > 0) {
                         // the first START closes the tail segment: park its aggregate
@@ -1084,16 +1084,16 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 double c;
                 if constexpr (ALG == 0) {
                     // 2. * atanh(rp / t) (:66-68) and the clip (:73-74) in one
-                    const double ra = rowA[r], tk = c2b.get(k);
+                    const double ra = rowA[r], tk = c2b.get_seq(k);
                     double prod;  // :66
                     if (div_fast) prod = ql_exact::div_rn_safe(ra, tk);
                     else prod = ra / tk;
                     c = ql_exact::atanh2_clip(prod, thr, a.spa_ctop);
                 } else if constexpr (SPA_FAM) {
-                    const double prod = rowA[r] / c2b.get(k);  // :66
+                    const double prod = rowA[r] / c2b.get_seq(k);  // :66
                     c = 2. * atanh_lin(prod);
                 } else {
-                    const double x = c2b.get(k);
+                    const double x = c2b.get_seq(k);
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
                     const double2 ab = row_ld(r);
                     const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
