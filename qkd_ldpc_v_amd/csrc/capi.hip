@@ -753,6 +753,31 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                 std::vector<int> ord(n);
                 for (int b = 0; b < n; ++b) ord[b] = b;
                 std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return dv[x] > dv[y]; });
+                // Thread t gathers positions t, t + T, ...: wave w's lanes take
+                // the 64-bit groups at j T + 64 w.  Groups of 64 consecutive
+                // bits in degree order (similar chunk counts: no lane idles
+                // long) are dealt longest-first to the wave with the least
+                // work so far, so the gather's barrier does not wait on the
+                // waves that drew the high-degree bits (QLDPC_VNG_DEAL=0: in
+                // order).  Only full rounds are dealt; the rest stays in order.
+                const int TW = g->T / 64, rounds = n / g->T;
+                if (env_int("QLDPC_VNG_DEAL", 1) && TW > 1 && rounds > 1) {
+                    const int ng = rounds * TW;
+                    std::vector<long long> load(TW, 0);
+                    std::vector<int> used(TW, 0), dst(ng);
+                    for (int gi = 0; gi < ng; ++gi) {  // groups come longest first
+                        const long long cost = (dv[ord[(size_t)gi * 64]] + 3) / 4;
+                        int best = -1;
+                        for (int w = 0; w < TW; ++w)
+                            if (used[w] < rounds && (best < 0 || load[w] < load[best])) best = w;
+                        dst[gi] = used[best]++ * g->T + 64 * best;
+                        load[best] += cost;
+                    }
+                    std::vector<int> dealt(ord);
+                    for (int gi = 0; gi < ng; ++gi)
+                        for (int l = 0; l < 64; ++l) dealt[dst[gi] + l] = ord[(size_t)gi * 64 + l];
+                    ord.swap(dealt);
+                }
                 vng_bits.resize((size_t)2 * n);
                 for (int i = 0; i < n; ++i) {
                     vng_bits[2 * i] = (uint32_t)ord[i];
