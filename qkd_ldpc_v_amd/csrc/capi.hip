@@ -90,6 +90,7 @@ struct DeviceGraph {
     int num_cus = 0;
     uint32_t *slot_meta = nullptr;
     int32_t *lane_row0 = nullptr, *lane_head = nullptr, *ell_col = nullptr, *row_deg = nullptr;
+    int32_t *wave_rows = nullptr;
     int32_t *lane_nst = nullptr, *lane_epl = nullptr;
     uint32_t *slot_meta_ms = nullptr;                  // V2 min-sum: rows listed by kpos
     uint64_t *vn_mask = nullptr, *vn_mask_ms = nullptr; // V2: [wave][dv_max] slot masks
@@ -404,14 +405,16 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
             return true;
         };
         // Rows partly in global scratch: the waves whose rows stay in LDS are
-        // the leading wl (as many as fit), and the others read a row from L2
-        // per message.  Those get a smaller share of a wave's edges so the
-        // phase barriers do not wait on them (R=0.5 code: 65% is 4.5% faster
-        // than an even deal, tools/c5_share_ab.sh) — the smallest share from
-        // QLDPC_RGLB_SHARE (percent) up whose deal fits the shape.  wl
-        // depends on the deal, so each deal is redone until they agree.
+        // the leading wl (as many as fit); the others write their rows to L2
+        // in the scan and read them back (the gather, and the copy their
+        // message pass reads).  Those get a smaller share of a wave's edges
+        // so the phase barriers do not wait on them (R=0.5 code: 80% is 4%
+        // faster than an even deal and 5% faster than 65%, tools/env_ab.sh)
+        // — the smallest share from QLDPC_RGLB_SHARE (percent) up whose deal
+        // fits the shape.  wl depends on the deal, so each deal is redone
+        // until they agree.
         bool ok = false;
-        const int share0 = rows_global ? std::min(100, std::max(10, env_int("QLDPC_RGLB_SHARE", 65))) : 100;
+        const int share0 = rows_global ? std::min(100, std::max(10, env_int("QLDPC_RGLB_SHARE", 80))) : 100;
         for (int sp = share0; sp <= 100 && !ok; sp += 5) ok = deal(sp / 100.0);
         if (!ok) continue;
         g.variant = VAR_V2;
@@ -974,7 +977,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
             (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
             (rc = upload(&dg->part_row0, g->part_row0)) ||
-            (rc = upload(&dg->lane_row0, lrow0)) ||
+            (rc = upload(&dg->lane_row0, lrow0)) || (rc = upload(&dg->wave_rows, g->wave_rows)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
             (rc = upload(&dg->row_deg, rdeg)) || (rc = upload(&dg->iso_bits, iso)) ||
@@ -1156,6 +1159,13 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.rows_wg_offset = (v2 && g->rows_global_ms && alg >= 2) ? v2_rows_offset(*g) : -1;
     a.rows_lds = (v2 && g->rows_global_ms && alg >= 2) ? g->rows_lds_ms : g->m;
     a.rows_lds_waves = (v2 && g->rows_global_ms && alg >= 2) ? g->rows_lds_waves_ms : (g->T / 64);
+    a.wave_rows = dg->wave_rows;
+    // the rows kept in global scratch fit the totals region below total[n]
+    // (dead between the scan and the bit gather): their waves' message pass
+    // reads them from an LDS copy (QLDPC_ROWS_COPY=0: from L2, A/B)
+    a.rows_copy = (a.rows_wg_offset >= 0 && (long long)(g->m - a.rows_lds) * 16 <= (long long)g->n * 8 &&
+                   env_int("QLDPC_ROWS_COPY", 1))
+                      ? 1 : 0;
     a.row_orig = dg->row_orig;
     a.col_orig = dg->col_orig;
     a.col_lab = dg->col_lab;
@@ -1382,6 +1392,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipDeviceSynchronize();
         (void)hipFree(d->slot_meta);
         (void)hipFree(d->lane_row0);
+        (void)hipFree(d->wave_rows);
         (void)hipFree(d->lane_head);
         (void)hipFree(d->lane_nst);
         (void)hipFree(d->slot_meta_ms);

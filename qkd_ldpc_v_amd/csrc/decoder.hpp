@@ -137,6 +137,8 @@ struct DecodeArgs {
     long long rows_wg_offset;
     int rows_lds;                   // ... of which the leading rows_lds layout rows stay in LDS (m: all)
     int rows_lds_waves;             // = the rows of waves 0 .. rows_lds_waves - 1
+    const int32_t *wave_rows;       // V2: first layout row of each wave (+ m)
+    int rows_copy;                  // ... the others' message pass reads an LDS copy of its rows
     // Bank-aware bit labels (relabel.cpp; one-workgroup register shapes): the
     // graph's metadata and the frame codes use labels, llr / bits / posterior
     // the reference's bit ids.  nullptr: identity.

@@ -225,7 +225,8 @@ typedef const __attribute__((address_space(4))) uint64_t cu64_t;
 // dependent FP64 back to back).  Rotating the favoured wave keeps them level.
 // A SIMD holds waves w, w + 4, w + 8, w + 12 of a workgroup, told apart by
 // w >> 2; the rotation runs backwards through them (measured: C2 SPA -5.6%,
-// C3 OMSA -3%, tools/ab_bench.sh).
+// C3 OMSA -3%, same-box A/B; also in the message pass and the VN phases:
+// C3 a further -1.6%, C5 R=0.5 -0.8%).
 __device__ __forceinline__ void rotate_prio(int g) {
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8));
     switch ((3 * g + wv) & 3) {
@@ -293,9 +294,7 @@ struct MetaSrcW : MetaSrc<R> {
         asm volatile("" : "+s"(epl_s));
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
-#ifdef QL_PRIO_MORE
             rotate_prio(g);
-#endif
             if (4 * g < epl_s) {
                 const auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, g * REG_TSTRIDE * 16, 0);
                 const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rs2, this->voff, g * REG_TSTRIDE * 16, 0);
@@ -312,9 +311,7 @@ struct MetaSrcW : MetaSrc<R> {
     __device__ __forceinline__ void each_group_masked(uint32_t mlo, uint32_t mhi, F &&f) const {
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
-#ifdef QL_PRIO_MORE
             rotate_prio(g);
-#endif
             const uint32_t w = (4 * g < 32) ? mlo : mhi;
             const uint32_t bits = (w >> ((4 * g) & 31)) & 15u;
             if (bits) {

@@ -98,6 +98,27 @@ constexpr int v2_tail_slots() { return S < 32 ? S : 32; }
 // SPLIT: a frame is decoded by a.split_k workgroups of one XCD (planner
 // parts: contiguous blocks of 16 waves' rows), which meet at every phase
 // boundary through a global arrival counter; totals are in global memory.
+// One 16-byte row aggregate {min1, min2} through a buffer resource.
+__device__ __forceinline__ double2 ld_row16(__amdgpu_buffer_rsrc_t rs, int r) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * 16, 0, 0);
+    double2 d;
+    d.x = __builtin_bit_cast(double, ((unsigned long long)v.y << 32) | v.x);
+    d.y = __builtin_bit_cast(double, ((unsigned long long)v.w << 32) | v.z);
+    return d;
+}
+__device__ __forceinline__ void st_row16(__amdgpu_buffer_rsrc_t rs, int r, double2 d) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const unsigned long long x = __builtin_bit_cast(unsigned long long, d.x);
+    const unsigned long long y = __builtin_bit_cast(unsigned long long, d.y);
+    u32x4 v;
+    v.x = (unsigned int)x;
+    v.y = (unsigned int)(x >> 32);
+    v.z = (unsigned int)y;
+    v.w = (unsigned int)(y >> 32);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, r * 16, 0, 0);
+}
+
 template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL);
@@ -197,15 +218,19 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // 0 .. a.rows_lds_waves - 1) stay in LDS, the others live in the
     // workgroup's global scratch.  A wave's scan and message pass touch only
     // its own rows, so there the choice is one scalar branch per access.
-    double2 *const rowAB_glb =
-        RGLB ? reinterpret_cast<double2 *>(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.rows_wg_offset)
-             : nullptr;
+    // The global rows are reached by buffer loads / stores only (a pointer
+    // select between them and LDS would become flat accesses; a buffer
+    // access past the m rows reads 0 and writes nothing).
+    const __amdgpu_buffer_rsrc_t rows_rs = __builtin_amdgcn_make_buffer_rsrc(
+        RGLB ? (void *)(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.rows_wg_offset) : (void *)a.scratch,
+        (short)0, RGLB ? a.m * 16 : 0, 0x00020000);
+    auto glb_ld = [&](int r) -> double2 { return ld_row16(rows_rs, r); };
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool rows_in_lds = !RGLB || wave < a.rows_lds_waves;
     auto row_ld = [&](int r) -> double2 {
         if constexpr (RGLB) {
             if (rows_in_lds) return rowAB_lds[r];
-            return rowAB_glb[r];
+            return glb_ld(r);
         } else {
             return rowAB[r];
         }
@@ -213,7 +238,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     auto row_st = [&](int r, double2 v) {
         if constexpr (RGLB) {
             if (rows_in_lds) rowAB_lds[r] = v;
-            else rowAB_glb[r] = v;
+            else st_row16(rows_rs, r, v);
         } else {
             rowAB[r] = v;
         }
@@ -605,7 +630,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                             for (int q = 0; q < 4; ++q)
                             {
                                 const int rq = (int)(((q < 2 ? cur.x : cur.y) >> (16 * (q & 1))) & 0xFFFFu);
-                                if constexpr (RGLB) ab[q] = (rq < a.rows_lds) ? rowAB_lds[rq] : rowAB_glb[rq];
+                                if constexpr (RGLB) ab[q] = (rq < a.rows_lds) ? rowAB_lds[rq] : glb_ld(rq);
                                 else ab[q] = rowAB[rq];
                             }
     #pragma unroll
@@ -1071,6 +1096,25 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             if (!compute) break;
 
             // ---- check-to-bit messages + VN phase 0 (total = llr + first message) ----
+            // RGLB: a wave whose rows live in global scratch copies them (just
+            // written by its own scan) into the totals region, which nothing
+            // reads until the bit gather rewrites it: its messages then read
+            // LDS.  A wave's message pass touches only its own rows, so no
+            // barrier; the gather still reads these rows from global.
+            // (row r >= rows_lds at rowcopy[r - rows_lds]: indices, never a
+            // pointer below the LDS block)
+            double2 *const rowcopy = reinterpret_cast<double2 *>(smem + V2_TOTAL_OFF);
+            if constexpr (RGLB) {
+                if (!rows_in_lds && a.rows_copy) {
+                    const int r0 = __builtin_amdgcn_readfirstlane(a.wave_rows[wave]);
+                    const int r1 = __builtin_amdgcn_readfirstlane(a.wave_rows[wave + 1]);
+                    for (int rr = r0 + lane; rr < r1; rr += 64) rowcopy[rr - a.rows_lds] = glb_ld(rr);
+                }
+            }
+            // (wave-uniform: the message pass's rows, one LDS pointer or L2)
+            const bool msg_glb = RGLB && !rows_in_lds && !a.rows_copy;
+            double2 *const rows_msg = (RGLB && !rows_in_lds) ? rowcopy : rowAB_lds;
+            const int msg_off = (RGLB && !rows_in_lds) ? a.rows_lds : 0;
             r = row0;
             // SPA on ROWSCAN shapes: the row counter by the scalar START mask
             // (v_addc; the min-sum message pass is too short to hide the load)
@@ -1095,7 +1139,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 } else {
                     const double x = c2b.get_seq(k);
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
-                    const double2 ab = row_ld(r);
+                    double2 ab;
+                    // (lanes without edges may hold any row: the index is clamped)
+                    if constexpr (RGLB) ab = msg_glb ? glb_ld(r) : rows_msg[max(r - msg_off, 0)];
+                    else ab = row_ld(r);
                     const bool eq1 = __builtin_fabs(x) == __builtin_fabs(ab.x);
                     c = ms_message(ab, xneg, eq1, msclip);
                     if constexpr (VNG_H) {
