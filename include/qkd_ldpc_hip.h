@@ -247,6 +247,16 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
  * device: frame build + decode + keys_match against the extended key (:1216). */
 typedef struct qldpc_rate_plan qldpc_rate_plan;
 int qldpc_xoshiro_state(uint64_t seed, uint64_t *state_out);
+/* qldpc_select_punctured_untainted: select_punctured_bits_untainted
+ * (src/array_and_matrix_operations.cpp:1002-1067, arXiv:1103.6149) — the
+ * untainted puncturing list get_punctured_bits_untainted (:1076-1123) writes
+ * to a missing .untp file, in selection order.  H as the flattened
+ * check_nodes (row_ptr/col_idx) and bit_nodes (col_ptr/row_idx) lists; draws
+ * from prng_state (advanced in place, as the reference's setup loop passes
+ * its generator).  punctured_out needs capacity n (NULL: count only). */
+int qldpc_select_punctured_untainted(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                                     const int32_t *col_ptr, const int32_t *row_idx, uint64_t *prng_state,
+                                     int32_t *punctured_out, int32_t *n_punctured);
 int qldpc_adapt_code_rate(int32_t n, int32_t m, double qber, double delta, double efficiency,
                           int32_t untainted_enabled, const int32_t *untainted, int32_t n_untainted,
                           uint64_t *prng_state, int32_t *punctured_out, int32_t *n_punctured, int32_t *shortened_out,

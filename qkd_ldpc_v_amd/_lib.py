@@ -84,6 +84,7 @@ _SIGNATURES = {
     "qldpc_bits_to_remove": (_I32, [_I32, _I32, _P, _P, _I32, _P, _I32, _P, _I32, _P, _PI32]),
     "qldpc_adapt_code_rate": (_I32, [_I32, _I32, ctypes.c_double, ctypes.c_double, ctypes.c_double, _I32, _P, _I32,
                                      _P, _P, _PI32, _P, _PI32, ctypes.POINTER(ctypes.c_double)]),
+    "qldpc_select_punctured_untainted": (_I32, [_I32, _I32, _P, _P, _P, _P, _P, _P, _PI32]),
     "qldpc_rate_plan_create": (_I32, [_P, _I32, _P, _I32, _P, ctypes.POINTER(_P)]),
     "qldpc_rate_plan_destroy": (None, [_P]),
     "qldpc_trials_rate_adapt_device": (_I32, [_I32, ctypes.c_double, _I32, _P, ctypes.c_uint64, _I32, _P, _P, _P,

@@ -1759,6 +1759,83 @@ int qldpc_adapt_code_rate(int32_t n, int32_t m, double qber, double delta, doubl
     return QLDPC_OK;
 }
 
+// ---- untainted puncturing (src/array_and_matrix_operations.cpp:975-1067) -----
+// select_punctured_bits_untainted (arXiv:1103.6149): while untainted bits
+// remain (X), take the bits of X with the fewest second-order neighbours
+// (bits sharing a check, the bit itself excluded: get_second_order_neighbors,
+// :975-996) inside X, in ascending order (std::set iteration), draw one with
+// uniform_int_distribution<size_t>(0, candidates - 1) from the caller's
+// generator, puncture it and remove it and its second-order neighbours from
+// X.  Same candidates, same draws, same order as the reference's set-scanning
+// loop; the counts |N2(i) n X| are kept incrementally instead of recounted
+// (the relation is symmetric, so removing r decrements every q in N2(r)).
+int qldpc_select_punctured_untainted(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                                     const int32_t *col_ptr, const int32_t *row_idx, uint64_t *prng_state,
+                                     int32_t *punctured_out, int32_t *n_punctured) {
+    if (n <= 0 || m < 0 || !row_ptr || !col_idx || !col_ptr || !row_idx || !prng_state || !n_punctured)
+        return fail(QLDPC_EINVAL, "bad dimensions or NULL arguments");
+    *n_punctured = 0;
+    if (row_ptr[m] != col_ptr[n]) return fail(QLDPC_EINVAL, "check_nodes / bit_nodes edge counts differ");
+    for (int j = 0; j < m; ++j)
+        for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e)
+            if (col_idx[e] < 0 || col_idx[e] >= n) return fail(QLDPC_EINVAL, "bit index out of range");
+    for (int i = 0; i < n; ++i)
+        for (int e = col_ptr[i]; e < col_ptr[i + 1]; ++e)
+            if (row_idx[e] < 0 || row_idx[e] >= m) return fail(QLDPC_EINVAL, "check index out of range");
+    // N2(i): sorted, unique, without i
+    std::vector<int64_t> n2p(n + 1, 0);
+    std::vector<int32_t> n2;
+    {
+        std::vector<int32_t> tmp;
+        for (int i = 0; i < n; ++i) {
+            tmp.clear();
+            for (int e = col_ptr[i]; e < col_ptr[i + 1]; ++e) {
+                const int j = row_idx[e];
+                tmp.insert(tmp.end(), col_idx + row_ptr[j], col_idx + row_ptr[j + 1]);
+            }
+            std::sort(tmp.begin(), tmp.end());
+            tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+            for (int32_t b : tmp)
+                if (b != i) n2.push_back(b);
+            n2p[i + 1] = (int64_t)n2.size();
+        }
+    }
+    Xoshiro256pp g(0);
+    for (int i = 0; i < 4; ++i) g.s[i] = prng_state[i];
+    std::vector<uint8_t> inx(n, 1);
+    std::vector<int32_t> cnt(n), xs(n), cand, punct;
+    for (int i = 0; i < n; ++i) cnt[i] = (int32_t)(n2p[i + 1] - n2p[i]);
+    for (int i = 0; i < n; ++i) xs[i] = i;  // X in ascending order (compacted lazily)
+    auto remove = [&](int r) {
+        if (!inx[r]) return;
+        inx[r] = 0;
+        for (int64_t q = n2p[r]; q < n2p[r + 1]; ++q) --cnt[n2[q]];
+    };
+    while (!xs.empty()) {
+        size_t w = 0;
+        int32_t min_n = n;  // (the reference starts its minimum at num_bit_nodes)
+        for (int32_t i : xs)
+            if (inx[i]) {
+                xs[w++] = i;
+                if (cnt[i] < min_n) min_n = cnt[i];
+            }
+        xs.resize(w);
+        if (xs.empty()) break;
+        cand.clear();
+        for (int32_t i : xs)
+            if (cnt[i] == min_n) cand.push_back(i);
+        std::uniform_int_distribution<size_t> d(0, cand.size() - 1);
+        const int chosen = cand[d(g)];
+        punct.push_back(chosen);
+        remove(chosen);
+        for (int64_t q = n2p[chosen]; q < n2p[chosen + 1]; ++q) remove(n2[q]);
+    }
+    for (int i = 0; i < 4; ++i) prng_state[i] = g.s[i];
+    *n_punctured = (int32_t)punct.size();
+    if (punctured_out) std::copy(punct.begin(), punct.end(), punctured_out);
+    return QLDPC_OK;
+}
+
 int qldpc_rate_plan_create(qldpc_graph *g, int32_t n_punct, const int32_t *punctured, int32_t n_short,
                            const int32_t *shortened, qldpc_rate_plan **out) {
     if (!g || !out) return fail(QLDPC_EINVAL, "graph / out is NULL");

@@ -1330,6 +1330,12 @@ bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
     return R == V2_R_SMALL && RG == V2_RG_HYBRID;  // + the host's LDS fit test
 }
 
+// Every one-workgroup register shape gets row_sem from the planner only when
+// its slot count fits the 63 slot bits of a row mask (capi.hip build_meta):
+// a larger shape would plan and then fail every launch below.
+static_assert(V2_R_TIGHT <= 63 && V2_R_SMALL <= 63 && V2_R_MID <= 63,
+              "register shapes without RG slots must have <= 63 slots (row_sem / row_rmask)");
+
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream) {
     // the scan of one-workgroup register frames reads the row structure masks
     // (plan_v2 only builds register shapes of <= 63 slots, which always get row_sem)

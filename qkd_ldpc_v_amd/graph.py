@@ -322,6 +322,25 @@ def adapt_code_rate(n: int, m: int, qber: float, delta: float, efficiency: float
     return p[:npn.value].copy(), s[:nsn.value].copy(), rate.value
 
 
+def select_punctured_untainted(H: "HMatrix", state) -> np.ndarray:
+    """select_punctured_bits_untainted (src/array_and_matrix_operations.cpp:
+    1002-1067): the untainted puncturing list in selection order — what the
+    reference writes to a missing .untp file (:1076-1123).  state: np.uint64[4]
+    generator state (xoshiro_state(seed)), advanced in place."""
+    import ctypes
+
+    if state is None:
+        raise ValueError("pass the generator state (xoshiro_state(seed))")
+    rp, ci = np.ascontiguousarray(H.row_ptr, np.int32), np.ascontiguousarray(H.col_idx, np.int32)
+    cp, ri = np.ascontiguousarray(H.col_ptr, np.int32), np.ascontiguousarray(H.row_idx, np.int32)
+    out = np.empty(H.n, np.int32)
+    cnt = ctypes.c_int32(0)
+    check(lib().qldpc_select_punctured_untainted(H.n, H.m, rp.ctypes.data, ci.ctypes.data, cp.ctypes.data,
+                                                  ri.ctypes.data, state.ctypes.data, out.ctypes.data,
+                                                  ctypes.byref(cnt)), "qldpc_select_punctured_untainted")
+    return out[:cnt.value].copy()
+
+
 def trials_rate_adapt_device(n: int, qber: float, seeds, n_punct: int, alice, bob, punct_alice, punct_bob,
                              seed_add: int = 0, stream=None) -> float:
     """trials_device plus QKD_LDPC_RATE_ADAPT's punctured draws (2 per position)."""

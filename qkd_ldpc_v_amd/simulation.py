@@ -15,7 +15,7 @@ Differences from the reference, by design: the matrix directory is given on
 the command line (the reference derives it from matrix_format under its source
 tree) and its *.mtrx files are taken in name order (the reference uses
 directory order, which the filesystem decides); the untainted-puncturing
-search for a missing .untp file is not restated (the file must exist);
+search for a missing .untp file runs and writes the file, as the reference's;
 throughput columns report the GPU pipeline's amortised per-trial time.
 """
 from __future__ import annotations
@@ -25,13 +25,14 @@ import ctypes
 import json
 import math
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 
 import numpy as np
 
 from ._lib import ALGORITHM_NAMES, Params, check, lib, log_p
-from .graph import Graph, adapt_code_rate, load_matrix, trial_seeds, xoshiro_state
+from .graph import Graph, adapt_code_rate, load_matrix, select_punctured_untainted, trial_seeds, xoshiro_state
 
 EPSILON = 1e-6  # src/config.hpp:199
 DEC_NAMES = {0: "SPA", 1: "SPA-LIN-APPROX", 2: "NMSA", 3: "OMSA", 4: "ANMSA", 5: "AOMSA"}
@@ -331,6 +332,33 @@ def _bits_to_remove(H, punct=None, short=None) -> int:
     return cnt.value
 
 
+def _punctured_bits_untainted(path: str, H, state) -> np.ndarray:
+    """get_punctured_bits_untainted (src/array_and_matrix_operations.cpp:
+    1076-1123): the first line of the .untp file next to the matrix; when it is
+    missing or empty, the untainted search (select_punctured_untainted, drawing
+    from the setup generator `state`) and the file written as the reference
+    writes it (indices separated by spaces, one line)."""
+    up = os.path.splitext(path)[0] + ".untp"
+    unt = np.empty(0, np.int32)
+    if os.path.exists(up):
+        with open(up) as f:
+            unt = np.array(f.readline().split(), np.int64)
+    for v in unt:
+        if v < 0 or v >= H.n:
+            raise ConfigError(f"The punctured bit index '{v}' is out of range [0,{H.n - 1}]. File: {up}")
+    if unt.size == 0:
+        print(f"WARNING: No file with punctured untainted bits found: {up} \nThis file will be automatically "
+              "created. Wait...", file=sys.stderr)
+        unt = select_punctured_untainted(H, state)
+        try:
+            with open(up, "w") as f:
+                f.write("".join(f"{int(v)} " for v in unt))
+        except OSError as e:
+            raise ConfigError(f"Unable to open file for writing: {up}") from e
+        print("File created successfully.", file=sys.stderr)
+    return unt.astype(np.int32)
+
+
 def prepare(cfg: Config, matrix_paths: list[str]):
     """prepare_sim_inputs (src/simulation.cpp:394-455): matrices + combinations."""
     state = xoshiro_state(cfg.simulation_seed)
@@ -342,13 +370,7 @@ def prepare(cfg: Config, matrix_paths: list[str]):
         if cfg.rate_adaptation:
             unt = None
             if cfg.untainted_puncturing:
-                up = os.path.splitext(path)[0] + ".untp"
-                if not os.path.exists(up):
-                    raise ConfigError(f"{up}: no untainted-puncturing list (generating one is not supported)")
-                with open(up) as f:
-                    unt = np.array(f.readline().split(), np.int32)
-                if unt.size and (unt.min() < 0 or unt.max() >= H.n):
-                    raise ConfigError(f"The punctured bit index is out of range [0,{H.n - 1}]. File: {up}")
+                unt = _punctured_bits_untainted(path, H, state)
             if cfg.use_adaptation_ranges:
                 deltas, effs = _adapt_ranges(cfg, rate)
                 pts = [(q, d, e) for q in _rate_qber_values(cfg, rate) for d in deltas for e in effs]

@@ -126,6 +126,38 @@ def test_rate_adapted_combinations_match_oracle_chain(tmp_path):
         assert c.bits_to_remove >= p.size + s.size
 
 
+def test_missing_untp_is_searched_and_written(tmp_path):
+    """get_punctured_bits_untainted (:1076-1123): no .untp -> the search runs on
+    the setup generator before the combinations' draws, and the file is
+    written (one line, indices each followed by a space) and read back next time."""
+    cfg = S.Config.load(cfg_path("adaptive_t"))
+    d = mtrx_dir(tmp_path, "c5_n10240_m2048.sp2")
+    mats, combos = S.prepare(cfg, S.matrix_files(d))
+    untp = [f for f in os.listdir(d) if f.endswith(".untp")]
+    assert len(untp) == 1
+    text = open(os.path.join(d, untp[0])).read()
+    H = load_fixture("c5_n10240_m2048.sp2")
+    st = Q.xoshiro_state(cfg.simulation_seed)
+    unt = Q.select_punctured_untainted(H, st)
+    assert text == "".join(f"{v} " for v in unt) and "\n" not in text
+    want = []
+    for m in cfg.adaptation_maps:
+        if m["code_rate"] != 0.805:
+            continue
+        p, s = P.adapt_code_rate(H.n, H.m, m["QBER"], m["delta"], m["efficiency"], unt, st)
+        if p.size or s.size:
+            want.append((m["QBER"], p, s))
+    assert len(combos) == len(want) > 0
+    for c, (q, p, s) in zip(combos, want):
+        assert c.config_qber == q and np.array_equal(c.punctured, p) and np.array_equal(c.shortened, s)
+    # second run: the written file is read, no search draws
+    mats2, combos2 = S.prepare(cfg, S.matrix_files(d))
+    st2 = Q.xoshiro_state(cfg.simulation_seed)
+    first = next(m for m in cfg.adaptation_maps if m["code_rate"] == 0.805)
+    p2, s2 = P.adapt_code_rate(H.n, H.m, first["QBER"], first["delta"], first["efficiency"], unt, st2)
+    assert np.array_equal(combos2[0].shortened, s2)
+
+
 def test_range_values_and_qber_buckets():
     assert S._range_values(0.01, 0.05, 0.01) == [0.01 + j * 0.01 for j in range(5)]
     assert S._range_values(0.3, 0.3, 0.1) == [0.3]

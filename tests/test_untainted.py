@@ -1,0 +1,163 @@
+"""Untainted puncturing search (select_punctured_bits_untainted,
+src/array_and_matrix_operations.cpp:975-1067; arXiv:1103.6149) — host code of
+the product library, CPU only.
+
+Pinning: the reference's .untp files (the lists it wrote with this search for
+the three format-3 codes, tests/golden/matrices/*.untp.gz) are replayed: every
+listed bit must be one of the minimum-count candidates of the untainted set
+at its step, and the set must empty exactly after the last one.  The
+generator state those files were written with is not recoverable (no config
+seed reproduces them from a fresh generator: the reference's setup loop
+shares one generator across matrices, src/simulation.cpp:373-397), so the
+draw sequence itself is checked against an independent numpy restatement
+with libstdc++'s uniform_int_distribution<size_t> (Lemire's nearly
+divisionless downscale over the oracle's raw Xoshiro256++ outputs).
+"""
+import gzip
+
+import numpy as np
+import pytest
+
+import qkd_ldpc_v_amd as Q
+from conftest import matrix_path
+from oracle import pyoracle as P
+
+CODES = ["c5_n10240_m2048", "c5b_n10240_m3584", "c5c_n10240_m5120"]
+
+
+def second_order(H):
+    """N2(i) as CSR: bits sharing a check with i, i excluded (:975-996)."""
+    rp, ci, cp, ri = (np.asarray(a, np.int64) for a in (H.row_ptr, H.col_idx, H.col_ptr, H.row_idx))
+    ptr, idx = [0], []
+    for i in range(H.n):
+        rows = ri[cp[i]:cp[i + 1]]
+        nb = np.unique(np.concatenate([ci[rp[j]:rp[j + 1]] for j in rows])) if rows.size else np.empty(0, np.int64)
+        nb = nb[nb != i]
+        idx.append(nb)
+        ptr.append(ptr[-1] + nb.size)
+    return np.asarray(ptr, np.int64), np.concatenate(idx) if idx else np.empty(0, np.int64)
+
+
+def counts_in_x(ptr, idx, inx):
+    """|N2(i) n X| for every i (the reference recounts them at every step)."""
+    s = np.concatenate([[0], np.cumsum(inx[idx].astype(np.int64))])
+    return s[ptr[1:]] - s[ptr[:-1]]
+
+
+def remove(ptr, idx, inx, cnt, b):
+    """X -= {b} u N2(b), keeping cnt = |N2(.) n X| (N2 is symmetric)."""
+    gone = np.concatenate([[b], idx[ptr[b]:ptr[b + 1]]])
+    gone = gone[inx[gone]]
+    inx[gone] = False
+    for r in gone:
+        np.subtract.at(cnt, idx[ptr[r]:ptr[r + 1]], 1)
+
+
+def replay(H, ptr, idx, chosen, recount_every=97):
+    """Every chosen bit is a minimum-count member of X at its step; X empties
+    exactly at the end.  -> the candidate index of each choice (the draws).
+    The counts are kept incrementally and recounted from scratch, as the
+    reference does at every step, every `recount_every` steps."""
+    inx = np.ones(H.n, bool)
+    cnt = counts_in_x(ptr, idx, inx)
+    draws = []
+    for k, b in enumerate(chosen):
+        assert inx.any(), f"X empty before choice {k}"
+        if k % recount_every == 0:
+            assert np.array_equal(cnt[inx], counts_in_x(ptr, idx, inx)[inx])
+        xs = np.flatnonzero(inx)
+        mn = cnt[xs].min()
+        cand = xs[cnt[xs] == mn]  # ascending: std::set iteration order
+        pos = np.searchsorted(cand, b)
+        assert pos < cand.size and cand[pos] == b, f"choice {k} (bit {b}) is not a minimum-count candidate"
+        draws.append((int(pos), int(cand.size)))
+        remove(ptr, idx, inx, cnt, int(b))
+    assert not inx.any(), "untainted bits left after the last choice"
+    return draws
+
+
+class LibstdcxxDraws:
+    """uniform_int_distribution<size_t>(0, k - 1) over a 64-bit generator in
+    libstdc++ 11: _S_nd (Lemire) with a 128-bit product."""
+
+    def __init__(self, seed, count=1 << 14):
+        self.raw = [int(v) for v in P.xoshiro(seed, count)]
+        self.i = 0
+
+    def _g(self):
+        v = self.raw[self.i]
+        self.i += 1
+        return v
+
+    def draw(self, k):
+        r = k  # urange + 1
+        prod = self._g() * r
+        low = prod & 0xFFFFFFFFFFFFFFFF
+        if low < r:
+            thr = ((1 << 64) - r) % r
+            while low < thr:
+                prod = self._g() * r
+                low = prod & 0xFFFFFFFFFFFFFFFF
+        return prod >> 64
+
+
+def restated_search(H, ptr, idx, seed):
+    d = LibstdcxxDraws(seed)
+    inx = np.ones(H.n, bool)
+    cnt = counts_in_x(ptr, idx, inx)
+    out = []
+    while inx.any():
+        xs = np.flatnonzero(inx)
+        cand = xs[cnt[xs] == cnt[xs].min()]
+        b = int(cand[d.draw(cand.size)])
+        out.append(b)
+        remove(ptr, idx, inx, cnt, b)
+    return np.asarray(out, np.int64)
+
+
+@pytest.fixture(scope="module", params=CODES)
+def code(request):
+    name = request.param
+    H = Q.load_matrix(matrix_path(name + ".sp2"), 3)
+    ptr, idx = second_order(H)
+    ref = np.array(gzip.open(matrix_path(name + ".untp")).read().split(), np.int64)
+    return name, H, ptr, idx, ref
+
+
+def test_reference_untp_lists_replay(code):
+    """The reference's own .untp lists follow the search rule step by step."""
+    name, H, ptr, idx, ref = code
+    draws = replay(H, ptr, idx, ref)
+    assert len(draws) == ref.size and ref.size == np.unique(ref).size
+
+
+def test_product_search_follows_the_rule_and_restatement(code):
+    name, H, ptr, idx, ref = code
+    seed = 5555  # configs/ADAPTIVE T.json's SIMULATION_SEED
+    st = Q.xoshiro_state(seed)
+    got = Q.select_punctured_untainted(H, st)
+    replay(H, ptr, idx, got)
+    assert np.array_equal(got, restated_search(H, ptr, idx, seed))
+    # the list is a maximal set of bits no two of which share a check's neighbourhood,
+    # of the same size class as the reference's (arXiv:1103.6149: ~10% of n here)
+    assert abs(got.size - ref.size) <= 0.05 * ref.size
+    # the generator advanced past the draws (chained calls continue from here)
+    assert not np.array_equal(st, Q.xoshiro_state(seed))
+
+
+def test_search_chains_generator_state():
+    H = Q.load_matrix(matrix_path("c5_n10240_m2048.sp2"), 3)
+    st = Q.xoshiro_state(777)
+    a = Q.select_punctured_untainted(H, st)
+    b = Q.select_punctured_untainted(H, st)  # continues from the advanced state
+    st2 = Q.xoshiro_state(777)
+    a2 = Q.select_punctured_untainted(H, st2)
+    assert np.array_equal(a, a2) and not np.array_equal(a, b)
+
+
+def test_search_rejects_bad_input():
+    H = Q.load_matrix(matrix_path("s1_n10_m5.sp1"), 2)
+    bad = Q.HMatrix(H.n, H.m, H.row_ptr, np.where(H.col_idx == 0, H.n, H.col_idx).astype(np.int32),
+                    H.col_ptr, H.row_idx, False)
+    with pytest.raises(Exception):
+        Q.select_punctured_untainted(bad, Q.xoshiro_state(1))
