@@ -1083,7 +1083,13 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         wgs = std::min(batch, dg->occ[alg] * dg->num_cus);
         // split frames: every workgroup of the device (each XCD must hold whole
         // part groups; the claim protocol needs >= split_k of them per XCD)
-        if (v2 && g->split_k > 1) wgs = dg->occ[alg] * dg->num_cus;
+        if (v2 && g->split_k > 1) {
+            wgs = dg->occ[alg] * dg->num_cus;
+            // QLDPC_SPLIT_WGS (A/B): fewer workgroups, so fewer frames share an
+            // XCD's L2 (whole XCD rounds of 8; every XCD keeps >= split_k)
+            const int lim = env_int("QLDPC_SPLIT_WGS", 0);
+            if (lim >= 8 * g->split_k && lim < wgs) wgs = lim - lim % 8;
+        }
         w = workspace(dg, stream);
         if (!w->counter) HIP_TRY(hipMalloc(&w->counter, 64));
         if (v2) {
