@@ -5,8 +5,10 @@ inject_errors, src/array_and_matrix_operations.cpp:889-933): Alice's key is
 i.i.d. Bernoulli(1/2); Bob's key is Alice's with exactly floor(n * QBER) bits
 flipped at distinct uniformly random positions; the accurate QBER is
 floor(n*QBER)/n.  This generator reproduces that distribution with numpy's
-PCG64 (seeded, vectorised over frames); the reference-identical Xoshiro256++
-stream is SURVEY §8(f)2 work.
+PCG64 (seeded, vectorised over frames) for tests and the smoke check; the
+reference-identical trials (Xoshiro256++ seeds, libstdc++ draw consumption)
+are `qkd_ldpc_v_amd.trials_device` / `trials_rate_adapt_device` (trials.hip),
+which bench.py and the simulation driver use.
 """
 from __future__ import annotations
 
