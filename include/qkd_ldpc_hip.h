@@ -77,16 +77,23 @@ int qldpc_load_matrix(const char *path, int32_t format, int32_t *n, int32_t *m, 
 /* ------------------------------------------------------------------ graph */
 
 /* Build the device-resident Tanner graph from check_nodes in CSR form
- * (row_ptr[m+1], col_idx[nnz]; bit ids of row j in ascending order).  The graph
- * is immutable, replicated on every device of device_mask (bit d = HIP device
- * d; 0 = current device only) and safe to share between host threads. */
+ * (row_ptr[m+1], col_idx[nnz]), bit_nodes taken as their ascending transpose.
+ * The graph is immutable, replicated on every device of device_mask (bit d =
+ * HIP device d; 0 = current device only) and safe to share between host
+ * threads.  Rows out of ascending order decode with the reference's occurrence
+ * pairing (see qldpc_graph_create_checked); a bit listed twice in one row
+ * returns QLDPC_EUNSUP. */
 int qldpc_graph_create(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
                        int32_t device_mask, qldpc_graph **out);
 
-/* As qldpc_graph_create, additionally checking that bit_nodes
- * (col_ptr[n+1], row_idx[nnz]) is the ascending transpose of check_nodes — the
- * pairing the reference's slot counters assume (src/qkd_ldpc_algorithm.cpp:
- * 67-69,116-118).  Unsorted or inconsistent lists return QLDPC_EUNSUP. */
+/* As qldpc_graph_create with the caller's bit_nodes (col_ptr[n+1],
+ * row_idx[nnz], the reference's H_matrix::bit_nodes in its own order).  When
+ * check_nodes rows are ascending and bit_nodes is their ascending transpose,
+ * the reference's slot counters (src/qkd_ldpc_algorithm.cpp:67-69,116-118) pair
+ * every message with its own edge; otherwise they pair an edge's b2c with
+ * another edge's message, and the graph decodes with that occurrence pairing
+ * (the v1 global-slot kernel and a pairing pass).  Lists that disagree on an
+ * edge count return QLDPC_EUNSUP. */
 int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr,
                                const int32_t *col_idx, const int32_t *col_ptr,
                                const int32_t *row_idx, int32_t device_mask, qldpc_graph **out);
@@ -166,7 +173,8 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
 
 /* Launch geometry the decoder uses for this graph on `device`: lanes per frame
  * (threads per workgroup), edges per lane, resident workgroups, dynamic LDS
- * bytes and the kernel variant name (static string). */
+ * bytes and the kernel variant name (static string).  A host-only graph
+ * (qldpc_graph_create_host) answers with workgroups == NULL. */
 int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, int32_t *lanes,
                      int32_t *edges_per_lane, int32_t *workgroups, int32_t *lds_bytes,
                      const char **variant);

@@ -107,6 +107,7 @@ struct DeviceGraph {
     uint64_t *row_rmask = nullptr;  // V2 scan: [row j][lane] slots of the lane's j-th started row
     int32_t *col_orig = nullptr, *col_lab = nullptr;  // V2 bank relabelling: label -> bit id, bit id -> label
     int32_t *ell_lab = nullptr;     // row-ELL in labels (the claim order reads label-ordered frame codes)
+    int32_t *pair_src = nullptr, *pair_col = nullptr;  // v1 occurrence pairing (unsorted adjacency), [k][lane]
     std::mutex mu;     // workspaces (ws), occupancy cache
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
@@ -172,6 +173,7 @@ struct qldpc_graph {
     std::vector<int> row_order;             // V2: layout row -> original row
     std::vector<int> layout_row_ptr;        // V2: row_ptr of the rows in layout order
     int vn_k0 = 0, n_hd = 0;                // V2 hybrid: first staged VN term, bits of degree > vn_k0
+    bool paired = false;                    // unsorted adjacency: v1 global-slot kernel with occurrence pairing
     int hd_uniform_dv = 0;                  // > 0: the staged bits are 0..n-1 in order, all of this degree
     int nst_max = 0;                        // V2 SPA scan: most rows started in one lane (row_rmask rows)
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
@@ -218,8 +220,9 @@ int round_up64(long long x) { return (int)(((x + 63) / 64) * 64); }
 void plan(qldpc_graph &g) {
     const long long E = g.E;
     const int dcm = std::max(1, g.max_dc);
-    // Register-resident messages: at most EPL_REG edges per lane.
-    if (dcm <= EPL_REG) {
+    // Register-resident messages: at most EPL_REG edges per lane.  (Occurrence
+    // pairing reads other lanes' messages: global-slot variants only.)
+    if (dcm <= EPL_REG && !g.paired) {
         const int T = std::max(64, round_up64((E + EPL_REG - 1) / EPL_REG));
         const int EPL = std::max((int)((E + T - 1) / T), dcm);
         if (T <= 1024 && EPL <= EPL_REG && lds_bytes_for(VAR_REG_LDS, g.n, g.m, T) <= LDS_LIMIT) {
@@ -530,8 +533,11 @@ std::vector<RelabelMemo> g_relabel_memo;  // most recent last, at most 8
 
 // host_only: plan and relabel without any device (introspection; the graph
 // has no devices and cannot decode).
+// bit_nodes (col_ptr / row_idx, the reference's H_matrix::bit_nodes in its
+// own order): NULL means the ascending transpose of check_nodes.
 int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx, int32_t device_mask,
-                qldpc_graph **out, bool host_only = false, const std::vector<int> *device_list = nullptr) {
+                qldpc_graph **out, bool host_only = false, const std::vector<int> *device_list = nullptr,
+                const int32_t *col_ptr = nullptr, const int32_t *row_idx = nullptr) {
     if (!out) return fail(QLDPC_EINVAL, "out is NULL");
     *out = nullptr;
     if (n <= 0 || m < 0 || !row_ptr || (!col_idx && row_ptr[m] > 0))
@@ -548,16 +554,61 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     g->m = m;
     g->E = E;
     std::vector<int> dv(n, 0);
+    bool rows_sorted = true;
     for (int j = 0; j < m; ++j) {
         g->max_dc = std::max(g->max_dc, row_ptr[j + 1] - row_ptr[j]);
         for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
             const int c = col_idx[e];
             if (c < 0 || c >= n) return fail(QLDPC_EINVAL, "col_idx entry out of range [0, n)");
-            if (e > row_ptr[j] && col_idx[e - 1] >= c)
-                return fail(QLDPC_EUNSUP, "check_nodes rows must list bit ids in strictly ascending order");
+            if (e > row_ptr[j] && col_idx[e - 1] >= c) rows_sorted = false;
             ++dv[c];
         }
     }
+    // The reference pairs a check's k-th input with the k-th time the VN loop
+    // visits that check (bit_pos_idx, src/qkd_ldpc_algorithm.cpp:116-118) and
+    // a bit's k-th message with the k-th check that reached it (check_pos_idx,
+    // :67-69).  With ascending check_nodes rows and bit_nodes their ascending
+    // transpose both pairings are the edge itself; otherwise an edge's b2c is
+    // total - c2b of the edge the counters pair it with (occurrence pairing).
+    if (!rows_sorted) {
+        for (int j = 0; j < m; ++j) {  // (a bit listed twice in one check is not supported)
+            std::vector<int32_t> r(col_idx + row_ptr[j], col_idx + row_ptr[j + 1]);
+            std::sort(r.begin(), r.end());
+            if (std::adjacent_find(r.begin(), r.end()) != r.end())
+                return fail(QLDPC_EUNSUP, "a check node lists the same bit twice");
+        }
+    }
+    bool cols_transpose = true;
+    if (col_ptr && row_idx) {
+        if (col_ptr[0] != 0 || col_ptr[n] != row_ptr[m])
+            return fail(QLDPC_EUNSUP, "bit_nodes and check_nodes hold different edge counts");
+        std::vector<int> cnt(m, 0);
+        for (int i = 0; i < n; ++i) {
+            if (col_ptr[i + 1] < col_ptr[i]) return fail(QLDPC_EINVAL, "col_ptr must be non-decreasing");
+            if (col_ptr[i + 1] - col_ptr[i] != dv[i])
+                return fail(QLDPC_EUNSUP, "bit_nodes and check_nodes disagree on a bit's degree");
+            for (int e = col_ptr[i]; e < col_ptr[i + 1]; ++e) {
+                const int j = row_idx[e];
+                if (j < 0 || j >= m) return fail(QLDPC_EINVAL, "row_idx entry out of range [0, m)");
+                ++cnt[j];
+            }
+        }
+        for (int j = 0; j < m; ++j)
+            if (cnt[j] != row_ptr[j + 1] - row_ptr[j])
+                return fail(QLDPC_EUNSUP, "bit_nodes and check_nodes disagree on a check's degree");
+        // bit_nodes[c] must list the checks holding c in ascending order (the
+        // order the check-node loop reaches c in) for the identity pairing
+        std::vector<int> fill(n, 0);
+        for (int j = 0; j < m && cols_transpose; ++j)
+            for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
+                const int c = col_idx[e];
+                if (row_idx[col_ptr[c] + fill[c]++] != j) {
+                    cols_transpose = false;
+                    break;
+                }
+            }
+    }
+    g->paired = !(rows_sorted && cols_transpose);
     for (int i = 0; i < n; ++i) g->dv_max = std::max(g->dv_max, dv[i]);
     {
         long long chunks = 0;
@@ -568,7 +619,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
     const char *want = std::getenv("QLDPC_VARIANT");
     const bool v1_only = want && std::strcmp(want, "v1") == 0;
-    if (v1_only || (!plan_v2(*g, row_ptr) && !plan_v2_split(*g, row_ptr))) plan(*g);
+    if (g->paired && want && std::strcmp(want, "v2") == 0)
+        return fail(QLDPC_EUNSUP, "QLDPC_VARIANT=v2 but the adjacency needs occurrence pairing (v1)");
+    if (v1_only || g->paired || (!plan_v2(*g, row_ptr) && !plan_v2_split(*g, row_ptr))) plan(*g);
     if (want && std::strcmp(want, "v2") == 0 && g->variant != VAR_V2)
         return fail(QLDPC_EUNSUP, "QLDPC_VARIANT=v2 but no V2 instantiation holds this graph");
     const int T = g->T, EPL = g->EPL;
@@ -896,6 +949,40 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         }
         return QLDPC_OK;
     };
+    // Occurrence pairing (unsorted adjacency, v1 global-slot layout: edge e at
+    // lane e / EPL, slot e % EPL, message index slot * T + lane).  The VN loop
+    // (:109-120) visits bit i's checks in bit_nodes order; its jj-th visit of
+    // check r fills r's next input slot with total[i] - c2b[i][jj], and
+    // c2b[i][jj] is the message of the jj-th check (in check order) holding i
+    // (:67-69).  pair_src / pair_col: per input slot, that message's index and i.
+    std::vector<int32_t> pair_src, pair_col;
+    if (g->paired) {
+        if (v2) return fail(QLDPC_EUNSUP, "occurrence pairing needs the v1 layout");
+        auto aidx = [&](int e) { return (e % EPL) * T + e / EPL; };
+        std::vector<int> cbase(n + 1, 0);
+        for (int i = 0; i < n; ++i) cbase[i + 1] = cbase[i] + dv[i];
+        std::vector<int> edge_of(E);  // (bit, occurrence rank) -> edge
+        for (int e = 0; e < E; ++e) edge_of[cbase[col_idx[e]] + kpos[e]] = e;
+        std::vector<int32_t> cp(cbase.begin(), cbase.end()), ri(E);
+        if (col_ptr && row_idx) {
+            cp.assign(col_ptr, col_ptr + n + 1);
+            ri.assign(row_idx, row_idx + E);
+        } else {  // bit_nodes = the ascending transpose
+            std::vector<int> fill(n, 0);
+            for (int j = 0; j < m; ++j)
+                for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) ri[cbase[col_idx[e]] + fill[col_idx[e]]++] = j;
+        }
+        pair_src.assign((size_t)EPL * T, 0);
+        pair_col.assign((size_t)EPL * T, 0);
+        std::vector<int> bpos(m, 0);
+        for (int i = 0; i < n; ++i)
+            for (int jj = 0; jj < dv[i]; ++jj) {
+                const int r = ri[cp[i] + jj];
+                const int e_dst = row_ptr[r] + bpos[r]++;
+                pair_src[aidx(e_dst)] = aidx(edge_of[cbase[i] + jj]);
+                pair_col[aidx(e_dst)] = i;
+            }
+    }
     std::vector<int32_t> row_orig(v2 ? g->row_order : std::vector<int>());
     g->vng = !vn_rows.empty();
     std::vector<uint32_t> meta_ms, meta2, meta2_ms;
@@ -985,6 +1072,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->vng_meta2, vng_meta2)) || (rc = upload(&dg->row_sem, row_sem)) ||
             (rc = upload(&dg->vng_rec, vng_rec)) ||
             (rc = upload(&dg->row_rmask, row_rmask)) ||
+            (g->paired && ((rc = upload(&dg->pair_src, pair_src)) || (rc = upload(&dg->pair_col, pair_col)))) ||
             (!col_orig.empty() && ((rc = upload(&dg->col_orig, col_orig)) || (rc = upload(&dg->col_lab, g->col_lab)) ||
                                    (rc = upload(&dg->ell_lab, ell_lab))))) {
             (void)hipSetDevice(prev);
@@ -1015,6 +1103,11 @@ int check_params(const qldpc_params *p) {
 // Hybrid min-sum with rows in global scratch: their offset (16-byte aligned).
 long long v2_rows_offset(const qldpc_graph &g) {
     return ((long long)g.v2RG * REG_TSTRIDE + g.stage_doubles + 1) / 2 * 2;
+}
+
+// v1: the kernel's scratch, plus (occurrence pairing) a slot-major b2c buffer
+long long v1_scratch_doubles(const qldpc_graph &g) {
+    return scratch_doubles_for(g.variant, g.n, g.m, g.T, g.EPL) + (g.paired ? (long long)g.EPL * g.T : 0);
 }
 
 long long v2_scratch_doubles(const qldpc_graph &g) {
@@ -1120,8 +1213,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
             w->order_frames = (size_t)batch;
         }
         {
-            const long long per = v2 ? v2_scratch_doubles(*g)
-                                     : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+            const long long per = v2 ? v2_scratch_doubles(*g) : v1_scratch_doubles(*g);
             const size_t need = (size_t)per * (size_t)wgs;
             if (need > w->scratch_doubles) {
                 if (w->scratch) {
@@ -1157,7 +1249,12 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.batch = batch; a.llr = llr; a.synd = synd; a.bits = bits; a.iters = iters; a.ok = ok; a.post = post;
     a.frame_counter = w->counter;
     a.scratch = w->scratch;
-    a.scratch_wg_doubles = v2 ? v2_scratch_doubles(*g) : scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    a.scratch_wg_doubles = v2 ? v2_scratch_doubles(*g) : v1_scratch_doubles(*g);
+    if (!v2 && g->paired) {
+        a.pair_src = dg->pair_src;
+        a.pair_col = dg->pair_col;
+        a.pair_buf_off = scratch_doubles_for(g->variant, g->n, g->m, g->T, g->EPL);
+    }
     a.hd_uniform_dv = g->hd_uniform_dv;
     a.vn_k0 = g->vn_k0; a.n_hd = g->n_hd; a.hd_bits = dg->hd_bits; a.hd_dv = dg->hd_dv; a.stage_off = dg->stage_off;
     a.slot_meta2 = (v2 && alg >= 2) ? dg->slot_meta2_ms : dg->slot_meta2;
@@ -1349,23 +1446,11 @@ int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr, con
                                const int32_t *col_ptr, const int32_t *row_idx, int32_t device_mask,
                                qldpc_graph **out) {
     if (!row_ptr || !col_idx || !col_ptr || !row_idx) return fail(QLDPC_EINVAL, "NULL adjacency array");
-    if (n <= 0 || m < 0 || col_ptr[n] != row_ptr[m])
-        return fail(QLDPC_EUNSUP, "bit_nodes and check_nodes hold different edge counts");
-    // bit_nodes must be the ascending transpose of check_nodes.
-    std::vector<int> fill(n, 0);
-    for (int i = 0; i < n; ++i)
-        if (col_ptr[i + 1] < col_ptr[i]) return fail(QLDPC_EINVAL, "col_ptr must be non-decreasing");
-    for (int j = 0; j < m; ++j)
-        for (int e = row_ptr[j]; e < row_ptr[j + 1]; ++e) {
-            const int c = col_idx[e];
-            if (c < 0 || c >= n) return fail(QLDPC_EINVAL, "col_idx entry out of range");
-            const int slot = col_ptr[c] + fill[c]++;
-            if (slot >= col_ptr[c + 1] || row_idx[slot] != j)
-                return fail(QLDPC_EUNSUP,
-                            "bit_nodes is not the ascending transpose of check_nodes: the reference's "
-                            "slot pairing would not match edges (unsorted adjacency)");
-        }
-    return build_graph(n, m, row_ptr, col_idx, device_mask, out);
+    if (n <= 0 || m < 0) return fail(QLDPC_EINVAL, "invalid graph dimensions");
+    // bit_nodes in the caller's order: anything but the ascending transpose of
+    // ascending check_nodes rows decodes with the reference's occurrence
+    // pairing (build_graph)
+    return build_graph(n, m, row_ptr, col_idx, device_mask, out, false, nullptr, col_ptr, row_idx);
 }
 
 int qldpc_graph_create_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
@@ -1420,6 +1505,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->vn_rows);
         (void)hipFree(d->vng_bits);
         (void)hipFree(d->vng_meta2);
+        (void)hipFree(d->pair_src);
+        (void)hipFree(d->pair_col);
         (void)hipFree(d->vng_rec);
         (void)hipFree(d->row_sem);
         (void)hipFree(d->row_rmask);
@@ -1461,7 +1548,8 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
     if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
     if (algorithm < 0 || algorithm > 5) return fail(QLDPC_EINVAL, "algorithm must be 0..5");
     DeviceGraph *dg = find_dev(const_cast<qldpc_graph *>(g), device);
-    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    // (a host-only graph answers everything but the device's workgroup count)
+    if (!dg && !(g->devs.empty() && !workgroups)) return fail(QLDPC_EINVAL, "graph does not live on that device");
     const size_t lds = lds_of(*g, algorithm);
     if (lanes) *lanes = g->T;
     if (edges_per_lane) *edges_per_lane = g->EPL;

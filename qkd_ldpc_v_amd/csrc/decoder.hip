@@ -82,6 +82,8 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
 
     EdgeMsgs<R> c2b;
     if constexpr (R == 0) c2b.bind(wg, tid, T);
+    // occurrence pairing (unsorted adjacency): global-slot instantiations only
+    double *const pbuf = (R == 0 && a.pair_src) ? wg + a.pair_buf_off : nullptr;
 
     MetaSrc<R> meta;
     meta.init(a.slot_meta, tid, T);
@@ -162,7 +164,10 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                 if (it == 0) {
                     x = llr[col];  // initial b2c = channel LLR, unclipped (:21-29)
                 } else {
-                    x = total[col] - c2b.get(k);  // VN extrinsic (:115)
+                    // VN extrinsic (:115); occurrence pairing: computed by the
+                    // pairing pass below from the edge the counters pair it with
+                    if (pbuf) x = pbuf[(size_t)k * T + tid];
+                    else x = total[col] - c2b.get(k);
                     if (thr_on) x = clip_msg(x, thr);
                 }
                 if constexpr (SPA_FAM) {
@@ -275,6 +280,20 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
                 STAMP(ST_VNK);
                 __syncthreads();
                 STAMP(ST_VNK_WAIT);
+            }
+            if constexpr (R == 0) {
+                // Occurrence pairing (:109-120 with unsorted lists): input slot s
+                // of the next check-node pass takes total[i] - c2b of the edge
+                // the reference's counters pair it with (another lane's slot).
+                // The messages stay untouched until the next scan, after the barrier.
+                if (pbuf) {
+                    meta.each(EPL, [&](int k, uint32_t mt) {
+                        if (!(mt & META_VALID)) return;
+                        const size_t s = (size_t)k * T + tid;
+                        pbuf[s] = total[a.pair_col[s]] - wg[a.pair_src[s]];
+                    });
+                    __syncthreads();
+                }
             }
             had_vn = true;
         }

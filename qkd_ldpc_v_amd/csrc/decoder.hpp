@@ -119,6 +119,13 @@ struct DecodeArgs {
     int *split_err;                 // set when a part group failed to meet (results void)
     double *gstage;                 // [batch][stage_frame_doubles] split frames' VN stage
     long long stage_frame_doubles;
+    // v1 global-slot kernels, unsorted adjacency (occurrence pairing): input
+    // slot s of the next check-node pass gets total[pair_col[s]] -
+    // c2b[pair_src[s]] (both [k][lane]); the values go through a slot-major
+    // buffer at pair_buf_off doubles into the workgroup's scratch.  nullptr: off.
+    const int32_t *pair_src;
+    const int32_t *pair_col;
+    long long pair_buf_off;
     // V2 min-sum bit gather (VNG, dv_max <= 4): the message pass records per
     // edge two bits (b2c <= 0, |b2c| == min1) in LDS, and one pass per bit
     // rebuilds its messages from its rows' aggregates and sums them in order.

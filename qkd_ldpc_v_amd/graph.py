@@ -91,6 +91,20 @@ class DecodeOutput:
     posterior: np.ndarray | None  # float64[batch, n] total_bit_llr
 
 
+def _canonical_adjacency(H: HMatrix) -> bool:
+    """check_nodes rows ascending and bit_nodes their ascending transpose: the
+    reference's slot pairing is then the edge itself (src/qkd_ldpc_algorithm.cpp:
+    67-69,116-118)."""
+    rp, ci = np.asarray(H.row_ptr), np.asarray(H.col_idx)
+    rows = np.repeat(np.arange(H.m, dtype=np.int64), np.diff(rp))
+    if ci.size and np.any((np.diff(ci) <= 0) & (rows[1:] == rows[:-1])):
+        return False
+    order = np.lexsort((rows, ci))
+    cp = np.zeros(H.n + 1, np.int64)
+    np.add.at(cp, ci.astype(np.int64) + 1, 1)
+    return np.array_equal(np.cumsum(cp), np.asarray(H.col_ptr)) and np.array_equal(rows[order], np.asarray(H.row_idx))
+
+
 class Graph:
     """A device-resident Tanner graph (qldpc_graph).
 
@@ -104,6 +118,11 @@ class Graph:
         self.H = H
         self.n, self.m = H.n, H.m
         g = ctypes.c_void_p()
+        if (host_only or devices is not None) and not _canonical_adjacency(H):
+            # (these entries take check_nodes only and assume bit_nodes is their
+            # ascending transpose; the reference's occurrence pairing of other
+            # lists needs qldpc_graph_create_checked)
+            raise ValueError("unsorted adjacency: use Graph(H) / Graph(H, device_mask=...)")
         if host_only:
             check(lib().qldpc_graph_create_host(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ctypes.byref(g)),
                   "qldpc_graph_create_host")

@@ -36,11 +36,14 @@ def test_version_and_log_p():
         assert Q.log_p(q) == math.log((1.0 - q) / q)
 
 
-def test_graph_rejects_unsorted_bit_nodes():
+def test_graph_rejects_inconsistent_bit_nodes():
+    """bit_nodes must list every edge of check_nodes (any order: the reference's
+    occurrence pairing, tests/test_unsorted.py); a column that names a check
+    twice instead of its two checks is refused."""
     H = HMatrix.from_check_nodes(4, [[0, 1, 2], [1, 2, 3]])
     ri = H.row_idx.copy()
     cp = H.col_ptr
-    ri[cp[1]:cp[2]] = ri[cp[1]:cp[2]][::-1]  # bit 1 lists checks [1, 0]
+    ri[cp[1]:cp[2]] = [1, 1]  # bit 1 lists check 1 twice
     bad = HMatrix(H.n, H.m, H.row_ptr, H.col_idx, cp, ri)
     with pytest.raises(QLDPCError, match="EUNSUP"):
         Q.Graph(bad)
