@@ -277,6 +277,19 @@ def test_c5_other_code_rates_all_algorithms(gpu_available, name, qber, alg, prim
     assert_parity(name, alg, prim, sec, qber=qber, batch=4, seed=70 + alg, max_it=2, thr_on=False)
 
 
+M2K = [("m2k_n10240_m1024.sp2", 0.006), ("m2k_n10240_m1536.sp2", 0.012), ("m2k_n10240_m2560.sp2", 0.028),
+       ("m2k_n10240_m3072.sp2", 0.036), ("m2k_n10240_m4096.sp2", 0.055), ("m2k_n10240_m4608.sp2", 0.065)]
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+@pytest.mark.parametrize("name,qber", M2K)
+def test_format3_codes_all_rates_all_algorithms(gpu_available, name, qber, alg, prim, sec):
+    """The other irregular format-3 codes the reference ships with untainted
+    lists (sparse_matrices/matrices_2_10k_all, R = 0.9 .. 0.55), whatever
+    shape the planner gives them."""
+    assert_parity(name, alg, prim, sec, qber=qber, batch=8, seed=80 + alg)
+
+
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
     assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"

@@ -3,7 +3,7 @@ src/array_and_matrix_operations.cpp:975-1067; arXiv:1103.6149) — host code of
 the product library, CPU only.
 
 Pinning: the reference's .untp files (the lists it wrote with this search for
-the three format-3 codes, tests/golden/matrices/*.untp.gz) are replayed: every
+the nine format-3 codes it ships, tests/golden/matrices/*.untp.gz) are replayed: every
 listed bit must be one of the minimum-count candidates of the untainted set
 at its step, and the set must empty exactly after the last one.  The
 generator state those files were written with is not recoverable (no config
@@ -22,7 +22,10 @@ import qkd_ldpc_v_amd as Q
 from conftest import matrix_path
 from oracle import pyoracle as P
 
-CODES = ["c5_n10240_m2048", "c5b_n10240_m3584", "c5c_n10240_m5120"]
+CODES = ["c5_n10240_m2048", "c5b_n10240_m3584", "c5c_n10240_m5120",  # sparse_matrices/matrices_2
+         # sparse_matrices/matrices_2_10k_all (its R=0.8/0.65/0.5 lists are the same files as above)
+         "m2k_n10240_m1024", "m2k_n10240_m1536", "m2k_n10240_m2560", "m2k_n10240_m3072", "m2k_n10240_m4096",
+         "m2k_n10240_m4608"]
 
 
 def second_order(H):

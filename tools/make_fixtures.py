@@ -16,6 +16,8 @@ import sys
 REF = "/root/reference/sparse_matrices"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden", "matrices")
 
+_M2K = [(1024, "0.9"), (1536, "0.85"), (2560, "0.75"), (3072, "0.7"), (4096, "0.6"), (4608, "0.55")]
+
 # fixture name -> (reference path relative to sparse_matrices/, format id, role)
 FIXTURES = {
     "c1_n1024_m220.alist": ("matrices_alist_1k_all/(N=1024,M=220,R=0.79,CW=5,SEED=444).mtrx", 1,
@@ -32,6 +34,12 @@ FIXTURES = {
     "c5b_n10240_m3584.untp": ("matrices_2/(N=10240,M=3584,R=0.65).untp", -1, "C5 sweep: R=0.65 untainted list"),
     "c5c_n10240_m5120.sp2": ("matrices_2/(N=10240,M=5120,R=0.5).mtrx", 3, "C5 sweep: format-3 irregular R=0.5"),
     "c5c_n10240_m5120.untp": ("matrices_2/(N=10240,M=5120,R=0.5).untp", -1, "C5 sweep: R=0.5 untainted list"),
+    # matrices_2_10k_all: the other format-3 codes with the reference's untainted lists
+    # (the R=0.8 / 0.65 / 0.5 files there are byte-identical to matrices_2's)
+    **{f"m2k_n10240_m{m}.sp2": (f"matrices_2_10k_all/(N=10240,M={m},R={r}).mtrx", 3,
+                                f"format-3 irregular R={r} (matrices_2_10k_all)") for m, r in _M2K},
+    **{f"m2k_n10240_m{m}.untp": (f"matrices_2_10k_all/(N=10240,M={m},R={r}).untp", -1,
+                                 f"R={r} untainted list (matrices_2_10k_all)") for m, r in _M2K},
     "kat_n6_m4.dense": ("matrices_uncompressed/(N=6,K=2,M=4,R=0.34).mtrx", 0, "Johnson Ex. 2.5 KAT matrix"),
     "u_n7_m3.dense": ("matrices_uncompressed/(N=7,K=4,M=3,R=0.57).mtrx", 0, "small uncompressed"),
     "u_n10_m5.dense": ("matrices_uncompressed/(N=10,K=5,M=5,R=0.5).mtrx", 0, "small uncompressed"),
