@@ -246,13 +246,14 @@ def main():
         kms = kernel_ms if kernel_ms else step_ms_stream
         achieved = (it_sum * B) / (kms * 1e-3) / 1e9
         traffic = None
-        valu_per_launch = None
+        valu_per_launch = valu_busy = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
             traffic = pm.get("hbm_bytes_per_launch")
             valu_per_launch = pm.get("valu_wave_instructions_per_launch")
+            valu_busy = pm.get("valu_busy_cycles_per_launch")
         res = {
             "metric": METRIC,
             "value": value,
@@ -297,13 +298,19 @@ def main():
         }
         if valu_per_launch:
             # The decode kernel keeps messages on chip: it is bound by FP64 VALU
-            # issue, not HBM.  VALU wave-instructions per launch from the PMC
-            # pass (profiles/pmc_<workload>.json) over this run's kernel time,
-            # against the whole-chip VALU issue rate tools/valu_bench.hip
-            # measures (profiles/r01/valu_microbench.json).
-            ach = valu_per_launch / (kms * 1e-3)
+            # issue, not HBM.  VALU issue cycles per launch from the PMC pass
+            # (profiles/pmc_<workload>.json: SQ_ACTIVE_INST_VALU, where a
+            # v_rcp_f64 counts 4 like its issue time; SQ_INSTS_VALU if absent)
+            # over this run's kernel time, against the whole-chip rate of
+            # full-rate VALU instructions tools/valu_bench.hip measures
+            # (profiles/r01/valu_microbench.json).
+            busy = valu_busy or valu_per_launch
+            ach = busy / (kms * 1e-3)
             res["compute_roofline"] = {"bound": "fp64-valu-issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR,
-                                       "unit": "wave-instructions/s", "frac": ach / VALU_PEAK_WAVE_INSTR}
+                                       "unit": "VALU issue cycles (full-rate wave-instruction slots)/s",
+                                       "frac": ach / VALU_PEAK_WAVE_INSTR,
+                                       "valu_wave_instructions_per_launch": valu_per_launch,
+                                       "valu_busy_cycles_per_launch": valu_busy}
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
                                                args.cpu_baseline_seconds, k_info,

@@ -62,14 +62,18 @@ def main(prof, tag, rnd="r03"):
             "WRITE_SIZE_KB": write,
             "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
             "valu_wave_instructions_per_launch": pmc.get("SQ_INSTS_VALU"),
+            # VALU issue cycles (SQ_ACTIVE_INST_VALU, quad-cycles): a
+            # transcendental FP64 op (v_rcp_f64) occupies the SIMD 4x as long
+            # as a full-rate op (= SQ_INSTS_VALU + 3 * SQ_INSTS_VALU_TRANS_F64)
+            "valu_busy_cycles_per_launch": pmc.get("SQ_ACTIVE_INST_VALU"),
         }
         if pmc.get("TCC_HIT_sum") is not None and pmc.get("TCC_MISS_sum") is not None:
             summ["l2_hit_rate"] = pmc["TCC_HIT_sum"] / max(1.0, pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"])
         if pmc.get("SQ_LDS_BANK_CONFLICT") is not None and pmc.get("SQ_ACTIVE_INST_LDS"):
             summ["lds_bank_conflict_per_active_lds"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_ACTIVE_INST_LDS"]
-        if summ["valu_wave_instructions_per_launch"] is None and os.path.exists(path):
-            # a partial pass set keeps the VALU count of the last full profile only if it is the same tag
-            summ.pop("valu_wave_instructions_per_launch")
+        for k in ("valu_wave_instructions_per_launch", "valu_busy_cycles_per_launch"):
+            if summ[k] is None:
+                summ.pop(k)
         with open(path, "w") as fh:
             json.dump(summ, fh, indent=1)
         print(wl, json.dumps(summ))
