@@ -895,6 +895,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
                         if (!v2) break;
                         wd = DUMMY;
                         if (sorted && vng_h) vng_meta2[midx(l, k)] = (uint32_t)((vng_chunks + li) * 4);
+                        // register-shape bit gather: dummy slots record into the
+                        // spare word past the per-bit bytes (V2Layout::syn)
+                        if (sorted && !vng_rec.empty()) vng_rec[midx(l, k)] = (uint32_t)((n + 3) & ~3);
                     } else {
                         const int j = lrow[e];
                         const int ed = perm[e];  // the edge at that position

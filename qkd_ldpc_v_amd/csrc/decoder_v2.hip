@@ -74,7 +74,9 @@ struct V2Layout {
         // (s << 31), in the palette-index area past the codes when it has room
         syn = 0;
         if (rowscan && !split) {
-            const size_t cs = V2_CODES_OFF + al16((size_t)n);
+            // (a spare word past the per-bit bytes: the min-sum bit gather's
+            // dummy slots OR their record bits into it)
+            const size_t cs = V2_CODES_OFF + al16((size_t)n + 4);
             if (cs + (size_t)m * 4 <= (size_t)V2_CODES_OFF + V2_CODES_CAP) {
                 syn = cs;
             } else {
@@ -485,14 +487,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // equal values, and a NaN ax leaves both unchanged exactly as the
         // reference's false compares do (IEEE minNum / maxNum return the
         // other operand).
-        // (v_min/v_max_f64 directly: no input here is a signalling NaN — ax
+        // (v_min/v_max_f64 directly: no input here is a signalling NaN — x
         // comes from arithmetic, m1 / m2 from DBL_MAX and these results — so
-        // the compiler's canonicalising copies for fminnum are dropped)
-        auto ms_push = [](double &m1, double &m2, double ax) {
+        // the compiler's canonicalising copies for fminnum are dropped; |x|
+        // is the instructions' abs source modifier, not a separate fabs)
+        auto ms_push = [](double &m1, double &m2, double x) {
             double t, u;
-            asm("v_min_f64 %0, %1, %2" : "=v"(t) : "v"(ax), "v"(m2));
+            asm("v_min_f64 %0, |%1|, %2" : "=v"(t) : "v"(x), "v"(m2));
             asm("v_max_f64 %0, %1, %2" : "=v"(u) : "v"(m1), "v"(t));
-            asm("v_min_f64 %0, %1, %2" : "=v"(t) : "v"(m1), "v"(ax));
+            asm("v_min_f64 %0, %1, |%2|" : "=v"(t) : "v"(m1), "v"(x));
             m2 = u;
             m1 = t;
         };
@@ -899,7 +902,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // agg_push (:381-397), branch-free; the count of negatives
                         // by v_addc (only its parity bit is ever read)
                         neg = add_carry(neg, 0, __builtin_amdgcn_ballot_w64(x < 0));
-                        ms_push(m1, m2, __builtin_fabs(x));
+                        ms_push(m1, m2, x);
                         if (__builtin_amdgcn_inverse_ballot_w64(emk)) {
                             // s xor parity(negatives) in min1's sign; the mismatch
                             // flag (ANMSA/AOMSA) is set after the loop
@@ -1010,7 +1013,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     neg = start ? 0 : neg;
                     // agg_push (:381-397), branch-free
                     neg ^= (x < 0) ? 1 : 0;
-                    ms_push(m1, m2, __builtin_fabs(x));
+                    ms_push(m1, m2, x);
                 }
                 cur_s = start ? s : cur_s;
                 sm = start ? (sm >> 1) : sm;
@@ -1139,6 +1142,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 } else {
                     const double x = c2b.get_seq(k);
                     const uint32_t xneg = (x > 0) ? 0u : 1u;
+                    // the two recorded bits: xneg | eq1 << 1, as one v_addc with
+                    // the xneg lane mask as carry-in (no select + or)
+                    auto rec2 = [&](bool eq1) -> uint32_t {
+                        return add_carry(eq1 ? 2u : 0u, 0u, __builtin_amdgcn_ballot_w64(!(x > 0)));
+                    };
                     double2 ab;
                     // (lanes without edges may hold any row: the index is clamped)
                     if constexpr (RGLB) ab = msg_glb ? glb_ld(r) : rows_msg[max(r - msg_off, 0)];
@@ -1149,17 +1157,15 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // the two bits at the edge's padded position (dummy slots:
                         // a scratch byte past the last chunk)
                         __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes) + (mt2 >> 4),
-                                              (xneg | (eq1 ? 2u : 0u)) << ((mt2 & 15u) * 2),
+                                              rec2(eq1) << ((mt2 & 15u) * 2),
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     } else if constexpr (VNG) {
                         // record the two bits the bit gather rebuilds this message
-                        // from, at the word and shift the host precomputed (mt2)
-                        const uint32_t kp = (mt >> META_KPOS_SHIFT) & META_KPOS_MASK;
-                        if (kp < 4u) {  // (dummy slots: kpos META_KPOS_MASK)
-                            __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes + (mt2 & 0xFFFFu)),
-                                                  (xneg | (eq1 ? 2u : 0u)) << (mt2 >> 16),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
+                        // from, at the word and shift the host precomputed (mt2;
+                        // dummy slots: the spare word past the codes, never read)
+                        __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(codes + (mt2 & 0xFFFFu)),
+                                              rec2(eq1) << (mt2 >> 16),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
