@@ -311,6 +311,13 @@ def main():
                                        "frac": ach / VALU_PEAK_WAVE_INSTR,
                                        "valu_wave_instructions_per_launch": valu_per_launch,
                                        "valu_busy_cycles_per_launch": valu_busy}
+            if alg >= 2:
+                # Min-sum: the (2E + 2n) * 8 B streaming model runs at or above
+                # 8 TB/s (C3: 1.05) because the kernel never streams messages,
+                # so it is no bound; the line's roofline is the binding one,
+                # VALU issue, and the byte model is kept beside it.
+                res["hbm_model_roofline"] = res["roofline"]
+                res["roofline"] = dict(res["compute_roofline"], traffic=traffic)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
                                                args.cpu_baseline_seconds, k_info,
