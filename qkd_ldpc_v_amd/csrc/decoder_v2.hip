@@ -176,6 +176,19 @@ __device__ __forceinline__ void group_sync(int *ctr, int target, int *err) {
 // kpos order onto the channel LLR (std::accumulate order, :78).
 // RGLB (hybrid min-sum bit gather only): the row aggregates live in the
 // workgroup's global scratch instead of LDS (a.rows_wg_offset).
+// LDS byte offset of total[col] for a slot's metadata word, col * 8, in one
+// v_mad_u32_u16 instead of a mask and a shift-add: whenever the totals live in
+// LDS the bit ids (dummy column n included) are below 2^16 — (n + 1) * 8
+// bytes fit 160 KiB, and launch_decode_v2 checks n < 2^16 — so the low 16
+// bits of the word are the bit id and its kpos / flag bits are ignored.
+// (base: the LDS address of total[0], the mad's addend)
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ lds_f64 *col_off8(uint32_t mt, uint32_t base) {
+    uint32_t o;
+    asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(o) : "v"(mt), "s"(base));
+    return (lds_f64 *)(uintptr_t)o;
+}
+
 template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false, bool RGLB = false>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -247,6 +260,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     };
     double *pal = reinterpret_cast<double *>(smem + V2_PAL_OFF);
     uint8_t *codes = smem + V2_CODES_OFF;
+    // total[bit id of metadata word mt] (LDS totals: by col_off8)
+    const uint32_t total_lds = (uint32_t)(uintptr_t)(lds_f64 *)(smem + V2_TOTAL_OFF);
+    auto tot_at = [&](uint32_t mt) -> auto & {
+        if constexpr (!SPLIT) return *col_off8(mt, total_lds);
+        else return total[(int)(mt & META_COL_MASK)];
+    };
 
     EdgeMsgsH<R, RG, RL> c2b;
     c2b.bind(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles, tid);
@@ -543,7 +562,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             if constexpr (!SPLIT && !VNG) {
                 if (__builtin_amdgcn_inverse_ballot_w64(vn_exec[k])) {  // kpos == 0
                     const int col = (int)(mt & META_COL_MASK);
-                    total[col] = llr_of(col) + c;  // first term of std::accumulate (:78)
+                    tot_at(mt) = llr_of(col) + c;  // first term of std::accumulate (:78)
                 }
             }
             if constexpr (GATHER) {
@@ -584,12 +603,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         // under the same mask)
                         asm("" : "=v"(tv[i]));
                         if (i < 4 * nv && __builtin_amdgcn_inverse_ballot_w64(em[i]))
-                            tv[i] = total[(int)((uint32_t)q[i / 4][i % 4] & META_COL_MASK)];
+                            tv[i] = tot_at((uint32_t)q[i / 4][i % 4]);
                     }
 #pragma unroll
                     for (int i = 0; i < NS; ++i)
                         if (i < 4 * nv && __builtin_amdgcn_inverse_ballot_w64(em[i]))  // kpos == kk
-                            total[(int)((uint32_t)q[i / 4][i % 4] & META_COL_MASK)] =
+                            tot_at((uint32_t)q[i / 4][i % 4]) =
                                 tv[i] + c2b.get((4 * g + i) < S ? 4 * g + i : 0);
                 });
                 STAMP(ST_VNK);
@@ -849,7 +868,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 // wait counter: a scalar load in flight would hold up the LDS wait)
                 uint64_t smk = sem[0], emk = sem[1], pmk = sem[2];
                 meta.each_upto(epl, [&](int k, uint32_t mt) {
-                    const double tv = total[(int)(mt & META_COL_MASK)];
+                    const double tv = tot_at(mt);
                     double b;
                     if constexpr (ALG == 0) b = tv - c2b.get(k);  // b2c = total - c2b (:115); +0 in iteration 0
                     else b = clip_msg(tv - c2b.get(k), thr_it);    // (:115, :122-123; :21-29)
@@ -1034,7 +1053,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             if constexpr (SPLIT) {  // totals in global memory: a group's four loads issued together
                 meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
             } else {
-                meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, total[(int)(mt & META_COL_MASK)]); });
+                meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, tot_at(mt)); });
             }
             // ---- rows split across two lanes of this wave: one shuffle ----
             {
@@ -1346,6 +1365,7 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     // the scan of one-workgroup register frames reads the row structure masks
     // (plan_v2 only builds register shapes of <= 63 slots, which always get row_sem)
     if (a.split_k <= 1 && a.v2RG == 0 && !a.row_sem) return hipErrorInvalidValue;
+    if (a.split_k <= 1 && a.n >= 0xFFFF) return hipErrorInvalidValue;  // col_off8: LDS totals, bit ids < 2^16
     if (a.vn_rows && !v2_vng_ok(a.alg, a.v2R, a.v2RG, a.split_k, a.dv_max, a.m)) return hipErrorInvalidValue;
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)

@@ -665,20 +665,20 @@ QL_HD double tanh_half_common(double b, uint32_t *ib_out) {
 
 // Table form of the per-class constants above.  They depend on k alone, and
 // the common path only reaches k in [-3, 63] (u in (-2, 0] or [2, 44)), so a
-// 67-entry table indexed by k + 3 holds X3, X4 and B and the exponent addend
-// k << 20, and also s_tanh.c's tail constant C: |x| >= 1 exactly when k > 0
-// (u >= 2 gives k >= 3, u in (-2, 0] gives k in [-3, 0]).  X3 and X4 are whole
-// doubles (a 16-byte LDS read lands them in register pairs: no assembly of hi
-// words over a zero low word); B and C as high words.  Same constants, same
-// IEEE operations as tanh_half_common.
-// An entry is a 16-byte A part (X3, X4) and a 16-byte B part (B, C, k << 20);
+// 67-entry table indexed by k + 3 holds X3, X4 and B, and also s_tanh.c's
+// tail constant C: |x| >= 1 exactly when k > 0 (u >= 2 gives k >= 3, u in
+// (-2, 0] gives k in [-3, 0]).  All four are whole doubles (16-byte LDS reads
+// land them in register pairs: no assembly of hi words over a zero low word);
+// the exponent addend k << 20 is one shift-add on the hi word.  Same
+// constants, same IEEE operations as tanh_half_common.
+// An entry is a 16-byte A part (X3, X4) and a 16-byte B part (B, C);
 // Expm1Tab::step is the entry stride in 16-byte units (2: A and B interleaved,
 // 32-byte entries — the decoder's layout; 1: two separate arrays).
 struct alignas(16) Expm1A {
     double x3, x4;
 };
 struct alignas(16) Expm1B {
-    uint32_t b_hi, c_hi, k20, pad;
+    double b, c;
 };
 struct Expm1Tab {
     const Expm1A *a;
@@ -696,10 +696,8 @@ QL_HD void expm1_class(int32_t k, Expm1A *ea, Expm1B *eb) {
     a_hi = (k == -1) ? 0xbff00000u : a_hi;
     ea->x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
     ea->x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
-    eb->b_hi = far ? 0xbff00000u : 0x80000000u;
-    eb->c_hi = big ? 0x3ff00000u : 0x80000000u;
-    eb->k20 = ku << 20;
-    eb->pad = 0;
+    eb->b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
+    eb->c = from_words(big ? 0x3ff00000u : 0x80000000u, 0u);
 }
 
 // tanh_half_common with the class constants from `tab` (EXPM1_CLASSES
@@ -721,8 +719,15 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     const uint32_t jb = hi_word(b);
     const uint32_t ib = jb & 0x7fffffffu;
     const bool big = ib >= 0x40000000u;
-    const double ab = __builtin_fabs(b);
-    const double u = big ? ab : -ab;
+    // u = +-|b| as |b| * (+-1): exact, one select and one multiply (the
+    // sign-word form the compiler would make of it needs an or, a select and
+    // a copy of the low word; |b| is the multiply's abs source modifier)
+#if defined(__HIP_DEVICE_COMPILE__)
+    double u;
+    asm("v_mul_f64 %0, |%1|, %2" : "=v"(u) : "v"(b), "v"(big ? 1.0 : -1.0));
+#else
+    const double u = big ? __builtin_fabs(b) : -__builtin_fabs(b);
+#endif
     double kf = invln2 * u + (big ? 0.5 : -0.5);
 #if !defined(__HIP_DEVICE_COMPILE__)
     kf = (kf > 1e6 || kf < -1e6 || kf != kf) ? 0.0 : kf;
@@ -752,9 +757,9 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
     // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
     // end (round-to-nearest is symmetric; the sum is never 0 on this path).
-    const double y = with_hi_word(ypre, hi_word(ypre) + cb.k20) + from_words(cb.b_hi, 0u);
+    const double y = with_hi_word(ypre, hi_word(ypre) + ((uint32_t)kc << 20)) + cb.b;
     const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
-    const double zp = from_words(cb.c_hi, 0u) + div_rn_safe(num, y + 2.0);
+    const double zp = cb.c + div_rn_safe(num, y + 2.0);
     *ib_out = ib;
     return __builtin_copysign(zp, b);
 }
