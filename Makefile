@@ -20,8 +20,9 @@ LIB := $(PKG)/libqkdldpc_hip.so
 ORACLE := oracle/libqkdldpc_oracle.so
 HOSTCHK := $(PKG)/host/host_mirror_check
 DROPIN := tests/dropin/run_trial_check
+BATCHCHK := tests/dropin/batch_check
 
-all: $(LIB) $(ORACLE) $(HOSTCHK) $(DROPIN)
+all: $(LIB) $(ORACLE) $(HOSTCHK) $(DROPIN) $(BATCHCHK)
 
 $(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -54,7 +55,7 @@ $(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/dec
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/decoder_v2_st.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
-$(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp include/qkd_ldpc_hip.h
+$(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp $(CSRC)/relabel.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi_st.o $(CSRC)/loaders.o $(CSRC)/relabel.o
 	mkdir -p $(PKG)/diag
@@ -63,16 +64,26 @@ $(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSR
 $(ORACLE): oracle/ldpc_oracle.c oracle/ldpc_oracle.h oracle/trials_oracle.cpp
 	$(MAKE) -C oracle
 
-$(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)
+$(HOSTCHK): $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp $(PKG)/host/qkd_ldpc_impl.hpp \
+            include/qkd_ldpc_hip.h $(LIB)
 	g++ -O2 -std=c++17 -Wall -I include $< -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/..' -o $@
 
 # The drop-in replacement TU for the reference's src/qkd_ldpc_algorithm.cpp,
 # compiled against the reference-shaped declarations of tests/dropin/api and
 # driven by a restatement of run_trial (tests/test_dropin.py).
-$(DROPIN): tests/dropin/run_trial_check.cpp $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp $(PKG)/host/qkd_ldpc_impl.hpp \
-           tests/dropin/api/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)
-	g++ -O2 -std=c++20 -Wall -I tests/dropin/api -I include tests/dropin/run_trial_check.cpp \
+$(DROPIN): tests/dropin/run_trial_check.cpp tests/dropin/trial_common.hpp $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp \
+           $(PKG)/host/qkd_ldpc_impl.hpp tests/dropin/api/qkd_ldpc_algorithm.hpp include/qkd_ldpc_hip.h $(LIB)
+	g++ -O2 -std=c++20 -Wall -pthread -I tests/dropin/api -I include tests/dropin/run_trial_check.cpp \
 	    $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -o $@
+
+# The batch seam: the drop-in TU for QKD_LDPC_batch_simulation (src/simulation.cpp:693-760)
+# beside the per-trial drop-in, driven by a restatement of the reference's loop pieces.
+BATCH_SRCS := tests/dropin/batch_check.cpp $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp $(PKG)/host/dropin/simulation_batch.cpp
+$(BATCHCHK): $(BATCH_SRCS) tests/dropin/trial_common.hpp $(PKG)/host/dropin/simulation_batch.hpp \
+             $(PKG)/host/qkd_ldpc_impl.hpp tests/dropin/api/qkd_ldpc_algorithm.hpp tests/dropin/api/simulation.hpp \
+             include/qkd_ldpc_hip.h $(LIB)
+	g++ -O2 -std=c++20 -Wall -pthread -I tests/dropin/api -I $(PKG)/host/dropin -I include $(BATCH_SRCS) \
+	    -L$(PKG) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN/../../$(PKG)' -o $@
 
 # FP64 VALU ceilings of the SPA edge math (tools/valu_bench.hip), run on the box.
 tools/valu_bench: tools/valu_bench.hip $(CSRC)/exact_math.h
@@ -80,7 +91,7 @@ tools/valu_bench: tools/valu_bench.hip $(CSRC)/exact_math.h
 valu_bench: tools/valu_bench
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK) $(DROPIN) $(STAMPLIB) tools/valu_bench
+	rm -f $(CSRC)/*.o $(LIB) $(HOSTCHK) $(DROPIN) $(BATCHCHK) $(STAMPLIB) tools/valu_bench
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean stamps valu_bench
@@ -115,10 +126,13 @@ $(ASAN)/libqkdldpc_oracle.so: oracle/ldpc_oracle.c oracle/ldpc_oracle.h oracle/t
 	$(LLVM_BIN)/clang++ -shared -shared-libsan $(SANFLAGS) $(ASAN)/ldpc_oracle.o $(ASAN)/trials_oracle.o -lm -lpthread -o $@
 $(ASAN)/host_mirror_check: $(PKG)/host/host_mirror_check.cpp $(PKG)/host/qkd_ldpc_algorithm.hpp $(PKG)/host/qkd_ldpc_impl.hpp $(ASAN)/libqkdldpc_hip.so
 	$(LLVM_BIN)/clang++ -O1 -std=c++17 -Wall $(SANFLAGS) -shared-libsan -I include $< -L$(ASAN) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN' -o $@
-$(ASAN)/run_trial_check: tests/dropin/run_trial_check.cpp $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp $(PKG)/host/qkd_ldpc_impl.hpp $(ASAN)/libqkdldpc_hip.so
-	$(LLVM_BIN)/clang++ -O1 -std=c++20 -Wall $(SANFLAGS) -shared-libsan -I tests/dropin/api -I include tests/dropin/run_trial_check.cpp \
+$(ASAN)/run_trial_check: tests/dropin/run_trial_check.cpp tests/dropin/trial_common.hpp $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp $(PKG)/host/qkd_ldpc_impl.hpp $(ASAN)/libqkdldpc_hip.so
+	$(LLVM_BIN)/clang++ -O1 -std=c++20 -Wall -pthread $(SANFLAGS) -shared-libsan -I tests/dropin/api -I include tests/dropin/run_trial_check.cpp \
 	    $(PKG)/host/dropin/qkd_ldpc_algorithm.cpp -L$(ASAN) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN' -o $@
-asan: $(ASAN)/libqkdldpc_hip.so $(ASAN)/libqkdldpc_oracle.so $(ASAN)/host_mirror_check $(ASAN)/run_trial_check
+$(ASAN)/batch_check: $(BATCH_SRCS) tests/dropin/trial_common.hpp $(PKG)/host/dropin/simulation_batch.hpp $(PKG)/host/qkd_ldpc_impl.hpp $(ASAN)/libqkdldpc_hip.so
+	$(LLVM_BIN)/clang++ -O1 -std=c++20 -Wall -pthread $(SANFLAGS) -shared-libsan -I tests/dropin/api -I $(PKG)/host/dropin -I include \
+	    $(BATCH_SRCS) -L$(ASAN) -lqkdldpc_hip -Wl,-rpath,'$$ORIGIN' -o $@
+asan: $(ASAN)/libqkdldpc_hip.so $(ASAN)/libqkdldpc_oracle.so $(ASAN)/host_mirror_check $(ASAN)/run_trial_check $(ASAN)/batch_check
 asan-check: asan
 	bash tools/asan_check.sh
 .PHONY: asan asan-check

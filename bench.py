@@ -171,7 +171,9 @@ def main():
     class Slot:  # per-stream frame workspace and outputs
         def __init__(self, s):
             self.stream = s
-            self.llr_ws = torch.empty((batch, n), dtype=torch.float64, device=dev)
+            # no f64 LLR workspace: the register decoders read the frame builder's
+            # palette codes, so the fused entry skips the LLR write (NULL llr_ws)
+            self.llr_ws = None
             self.syn_ws = torch.empty((batch, m), dtype=torch.uint8, device=dev)
             self.bits = torch.empty((batch, n), dtype=torch.uint8, device=dev)
             self.iters = torch.empty(batch, dtype=torch.int32, device=dev)
@@ -321,7 +323,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(H, alg, prim, sec, qber, args.max_iterations,
                                                args.cpu_baseline_seconds, k_info,
-                                               SIMULATION_SEEDS.get(args.workload, 1022025) + 1)
+                                               SIMULATION_SEEDS.get(args.workload, 1022025) + 1,
+                                               (punct, short) if ra else None)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()
@@ -384,12 +387,13 @@ def host_cpus():
     return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": usable, "model": model}
 
 
-def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info, seed):
+def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info, seed, rate_adapt=None):
     """The CPU oracle (a port of the reference decoder, glibc math, one frame per
     task on a thread pool like src/simulation.cpp:721,740-746) on a bounded
     sample of the same workload: chunks of frames until `seconds` elapse, on
     every host CPU this job may use (value), then on one thread (value_1thread,
-    a third of the time budget)."""
+    a third of the time budget).  rate_adapt = (punctured, shortened): the
+    frames are QKD_LDPC_RATE_ADAPT's extended frames, as on the GPU."""
     from oracle import pyoracle as P
     from oracle.pyoracle import Oracle
 
@@ -402,13 +406,20 @@ def cpu_baseline(H, alg, prim, sec, qber, max_it, seconds, k_info, seed):
         chunk = threads * 4
         frames, t_dec = 0, 0.0
         while t_dec < budget and start + frames + chunk <= seeds.size:
-            tr = [P.trial(H.n, qber, int(sd)) for sd in seeds[start + frames:start + frames + chunk]]  # untimed
-            a = np.stack([t[0] for t in tr])
-            b = np.stack([t[1] for t in tr])
-            q = tr[0][2]
-            t0 = time.perf_counter()
-            lp = math.log((1.0 - q) / q)
-            llr = np.where(b != 0, -lp, lp)
+            sds = seeds[start + frames:start + frames + chunk]
+            if rate_adapt is None:
+                tr = [P.trial(H.n, qber, int(sd)) for sd in sds]  # untimed
+                a = np.stack([t[0] for t in tr])
+                b = np.stack([t[1] for t in tr])
+                q = tr[0][2]
+                t0 = time.perf_counter()
+                lp = math.log((1.0 - q) / q)
+                llr = np.where(b != 0, -lp, lp)
+            else:  # the extended frame (its LLRs come with the draws; the build is O(n) either way)
+                tr = [P.trial_rate_adapt(H.n, qber, int(sd), rate_adapt[0], rate_adapt[1]) for sd in sds]
+                a = np.stack([t[0] for t in tr])
+                llr = np.stack([t[1] for t in tr])
+                t0 = time.perf_counter()
             s = H.syndrome(a)
             bits, it, ok, _ = O.decode_batch(p, llr, s, threads=threads)
             (bits == a).all(axis=1)

@@ -105,6 +105,13 @@ int qldpc_graph_create_checked(int32_t n, int32_t m, const int32_t *row_ptr,
 int qldpc_graph_create_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
                           const int32_t *devices, int32_t ndevices, qldpc_graph **out);
 
+/* qldpc_graph_create_checked on an explicit device list (one shard per entry,
+ * as qldpc_graph_create_on): the C++ drop-in's graphs (the node's GPUs, or
+ * logical shards of one GPU for tests). */
+int qldpc_graph_create_checked_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                                  const int32_t *col_ptr, const int32_t *row_idx, const int32_t *devices,
+                                  int32_t ndevices, qldpc_graph **out);
+
 /* Plan only, on the host (no device is touched): the returned graph has no
  * devices and cannot decode; it answers qldpc_graph_info and
  * qldpc_graph_labels.  For inspection and CPU tests of the planner. */
@@ -161,8 +168,11 @@ int qldpc_keys_match_device(int32_t batch, int32_t n, const uint8_t *d_alice,
                             const uint8_t *d_bits, uint8_t *d_keys_match, void *stream);
 
 /* The whole per-trial window of QKD_LDPC for `batch` trials on device: frame
- * construction + decode + key comparison.  d_llr_ws / d_synd_ws: caller-owned
- * workspaces of batch*n doubles and batch*m bytes. */
+ * construction + decode + key comparison.  d_synd_ws: caller-owned workspace
+ * of batch*m bytes (Alice's syndromes).  d_llr_ws: batch*n doubles or NULL —
+ * when given, the frames' LLRs are written there; NULL skips them where the
+ * graph's decoder reads the frame builder's palette codes instead (the
+ * register kernels), and uses an internal workspace otherwise. */
 int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_params *p,
                                 int32_t batch, const uint8_t *d_alice, const uint8_t *d_bob,
                                 const double *d_log_p, double *d_llr_ws, uint8_t *d_synd_ws,
@@ -218,6 +228,10 @@ const char *qldpc_last_error(void);
 /* Library version string. */
 const char *qldpc_version(void);
 
+/* Number of HIP devices visible to the process (the C++ drop-in's default
+ * device list: every GPU of the node). */
+int qldpc_device_count(int32_t *count);
+
 /* ---- Trial generator ------------------------------------
  * qldpc_trial_seeds: the simulation loop's per-trial seeds — `count` draws of
  * uniform_int_distribution<size_t>(0, SIZE_MAX) over Xoshiro256PlusPlus(
@@ -252,7 +266,8 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
  * Alice's extended key [batch*n], LLRs (+-log_p / 1e-4 / DBL_MAX) [batch*n]
  * and Alice's syndrome [batch*m].
  * qldpc_qkd_ldpc_rate_adapt_batch_device: QKD_LDPC_RATE_ADAPT's window on
- * device: frame build + decode + keys_match against the extended key (:1216). */
+ * device: frame build + decode + keys_match against the extended key (:1216);
+ * d_llr_ws nullable as in qldpc_qkd_ldpc_batch_device. */
 typedef struct qldpc_rate_plan qldpc_rate_plan;
 int qldpc_xoshiro_state(uint64_t seed, uint64_t *state_out);
 /* qldpc_select_punctured_untainted: select_punctured_bits_untainted
@@ -300,6 +315,32 @@ int qldpc_sort_permutation(const double *keys, int32_t n, int32_t *perm_out);
 int qldpc_bits_to_remove(int32_t n, int32_t m, const int32_t *col_ptr, const int32_t *row_idx, int32_t n_punct,
                          const int32_t *punctured, int32_t n_short, const int32_t *shortened, int32_t rate_adapt,
                          int32_t *out, int32_t *count);
+
+/* ---- The simulation loop's batch seam --------------
+ * qldpc_run_trials: run_trial for `count` trials of one combination
+ * (src/simulation.cpp:540-576) — the body of QKD_LDPC_batch_simulation's
+ * pool.detach_loop(0, TRIALS_NUMBER) (:721-746) — with host pointers only.
+ * Trial t: a generator seeded with seeds[t] + seed_add (the loop's
+ * `seeds[n] + curr_sim`), Alice = fill_random_bits, Bob = inject_errors
+ * (src/array_and_matrix_operations.cpp:889-933), then QKD_LDPC (plan == NULL,
+ * src/qkd_ldpc_algorithm.cpp:1031-1119) or QKD_LDPC_RATE_ADAPT with the plan's
+ * punctured / shortened positions (:1121-1258, the punctured draws continuing
+ * from the same generator).  Everything happens on device: only the seeds go
+ * in and {iterations_num, syndromes_match, keys_match} per trial come back.
+ * The trials are split in contiguous slices over the graph's devices, one
+ * host thread each, no collectives; on each device chunks alternate over two
+ * streams so the next chunk's trials are generated while one decodes.
+ * runtime_us_out (nullable): trial_result::runtime — the measured duration of
+ * the trial's chunk window (frame build + decode + key compare; trial
+ * generation excluded, as :559-568 time only the QKD_LDPC call) shared out
+ * over the chunk's trials in proportion to each trial's own decode span (its
+ * frame's claim-to-result time on the GPU).  accurate_qber_out (nullable):
+ * floor(n * qber) / n, every trial's trial_result::accurate_QBER.
+ * Errors: QLDPC_EINVAL with run_trial's message when floor(n * qber) == 0. */
+int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber,
+                     int32_t count, const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out,
+                     uint8_t *synd_ok_out, uint8_t *keys_match_out, double *runtime_us_out,
+                     double *accurate_qber_out);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,7 @@ _SIGNATURES = {
     "qldpc_graph_create": (_I32, [_I32, _I32, _P, _P, _I32, ctypes.POINTER(_P)]),
     "qldpc_graph_create_checked": (_I32, [_I32, _I32, _P, _P, _P, _P, _I32, ctypes.POINTER(_P)]),
     "qldpc_graph_create_on": (_I32, [_I32, _I32, _P, _P, _P, _I32, ctypes.POINTER(_P)]),
+    "qldpc_graph_create_checked_on": (_I32, [_I32, _I32, _P, _P, _P, _P, _P, _I32, ctypes.POINTER(_P)]),
     "qldpc_graph_create_host": (_I32, [_I32, _I32, _P, _P, ctypes.POINTER(_P)]),
     "qldpc_graph_labels": (_I32, [_P, _P, _P]),
     "qldpc_graph_destroy": (None, [_P]),
@@ -94,6 +95,9 @@ _SIGNATURES = {
                                                       _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "qldpc_trials_device": (_I32, [_I32, ctypes.c_double, _I32, _P, ctypes.c_uint64, _P, _P,
                                    ctypes.POINTER(ctypes.c_double), _P]),
+    "qldpc_run_trials": (_I32, [_P, _P, ctypes.POINTER(qldpc_params), ctypes.c_double, _I32, _P, ctypes.c_uint64,
+                                _P, _P, _P, _P, ctypes.POINTER(ctypes.c_double)]),
+    "qldpc_device_count": (_I32, [_PI32]),
     "qldpc_last_error": (ctypes.c_char_p, []),
     "qldpc_version": (ctypes.c_char_p, []),
 }

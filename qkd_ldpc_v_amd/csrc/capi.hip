@@ -68,10 +68,10 @@ struct Workspace {  // per (device, stream): frame counter + decoder scratch
     int32_t *fweight = nullptr, *forder = nullptr;
     size_t order_frames = 0;
     int order_count = 0;  // frames of the last decode claimed through forder (0: index order)
-    // relabelled graphs, frames from llr[] (palettize): the llr of frames the
-    // palette cannot hold, in label order (batch x n; allocated on first need)
-    double *llr_lab = nullptr;
-    size_t llr_lab_frames = 0;
+    // the fused entries' frame LLRs when the caller passes no workspace and the
+    // graph's decoder reads llr[] (not V2), capacity in frames
+    double *llr_ws = nullptr;
+    size_t llr_ws_frames = 0;
     // kernel timing (qldpc_set_kernel_timing): events around the last decode launch
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_recorded = false;
@@ -83,6 +83,25 @@ struct HostIO {  // device staging buffers of the host-buffer entry
     uint32_t *iters = nullptr;
     size_t cap_frames = 0;
     hipStream_t stream = nullptr;
+};
+
+// qldpc_run_trials: one pipeline slot of a device's trial batches — the
+// chunk's seeds, keys and results on device, its results in pinned host memory
+// (two slots per device: chunk c + 1's trials are generated while chunk c
+// decodes on the other stream).
+struct TrialSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint64_t *seeds = nullptr, *clk = nullptr;
+    uint8_t *alice = nullptr, *bob = nullptr, *palice = nullptr, *pbob = nullptr, *alice_ext = nullptr;
+    uint8_t *synd = nullptr, *bits = nullptr, *ok = nullptr, *km = nullptr;
+    uint32_t *iters = nullptr, *tscratch = nullptr;
+    double *logp = nullptr;
+    uint32_t *h_iters = nullptr;
+    uint8_t *h_ok = nullptr, *h_km = nullptr;
+    uint64_t *h_clk = nullptr;
+    size_t cap = 0, cap_punct = 0;
+    int f0 = 0, nb = 0;  // the chunk in flight (nb == 0: none)
 };
 
 struct DeviceGraph {
@@ -112,6 +131,8 @@ struct DeviceGraph {
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
     HostIO io;
+    std::mutex trial_mu;  // qldpc_run_trials' pipeline slots, held for a whole call
+    TrialSlot tslot[2];
     int occ[6] = {0, 0, 0, 0, 0, 0};
 };
 
@@ -1113,10 +1134,20 @@ long long v1_scratch_doubles(const qldpc_graph &g) {
     return scratch_doubles_for(g.variant, g.n, g.m, g.T, g.EPL) + (g.paired ? (long long)g.EPL * g.T : 0);
 }
 
-long long v2_scratch_doubles(const qldpc_graph &g) {
-    if (g.split_k > 1) return 32;  // the stage is per frame (Workspace::gstage)
+// Relabelled graphs: a non-paletted frame's llr[] in label order, per workgroup
+// (DecodeArgs::llr_lab_wg_offset), after everything else; -1: not relabelled.
+long long v2_llr_lab_offset(const qldpc_graph &g) {
+    if (g.split_k > 1 || g.col_lab.empty()) return -1;
     const long long end = g.rows_global_ms ? v2_rows_offset(g) + 2LL * g.m
                                            : (long long)g.v2RG * REG_TSTRIDE + g.stage_doubles;
+    return (end + 31) / 32 * 32;
+}
+
+long long v2_scratch_doubles(const qldpc_graph &g) {
+    if (g.split_k > 1) return 32;  // the stage is per frame (Workspace::gstage)
+    long long end = g.rows_global_ms ? v2_rows_offset(g) + 2LL * g.m
+                                     : (long long)g.v2RG * REG_TSTRIDE + g.stage_doubles;
+    if (v2_llr_lab_offset(g) >= 0) end = v2_llr_lab_offset(g) + g.n;
     return (end + 31) / 32 * 32;
 }
 
@@ -1160,7 +1191,7 @@ int split_check(qldpc_graph *g, DeviceGraph *dg, hipStream_t stream) {
 // when `codes_ready` (written by build_frames), else computed here from llr.
 int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch, const double *llr,
               const uint8_t *synd, uint8_t *bits, uint32_t *iters, uint8_t *ok, double *post,
-              hipStream_t stream, bool codes_ready = false) {
+              hipStream_t stream, bool codes_ready = false, uint64_t *frame_clk = nullptr) {
     if (batch == 0) return QLDPC_OK;
     const int alg = p->algorithm;
     const bool v2 = g->variant == VAR_V2;
@@ -1275,6 +1306,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.row_orig = dg->row_orig;
     a.col_orig = dg->col_orig;
     a.col_lab = dg->col_lab;
+    a.llr_lab_wg_offset = (v2 && dg->col_orig) ? v2_llr_lab_offset(*g) : -1;
+    a.frame_clk = frame_clk;
     a.row_sem = (v2 && g->nst_max > 0) ? dg->row_sem : nullptr;
     a.row_rmask = (v2 && g->nst_max > 0) ? dg->row_rmask : nullptr;
     a.nst_max = g->nst_max;
@@ -1312,26 +1345,8 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         if (a.rows_wg_offset >= 0 && !a.vn_rows)
             return fail(QLDPC_EUNSUP, "this code's min-sum row aggregates need the bit gather (QLDPC_VNG=0 given)");
     }
-    if (v2 && !codes_ready) {
-        // relabelled graphs read a non-paletted frame's llr[] by label: palettize
-        // writes those frames' LLRs in label order into the workspace
-        double *llr_lab = nullptr;
-        if (dg->col_orig) {
-            std::lock_guard<std::mutex> lk(dg->mu);
-            if ((size_t)batch > w->llr_lab_frames) {
-                HIP_TRY(hipStreamSynchronize(stream));
-                (void)hipFree(w->llr_lab);
-                w->llr_lab = nullptr;
-                w->llr_lab_frames = 0;
-                HIP_TRY(hipMalloc(&w->llr_lab, (size_t)batch * g->n * sizeof(double)));
-                w->llr_lab_frames = (size_t)batch;
-            }
-            llr_lab = w->llr_lab;
-            a.llr = llr_lab;
-        }
-        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, dg->col_orig, llr_lab,
-                                 stream));
-    }
+    if (v2 && !codes_ready)  // (relabelled graphs: the kernel reads a non-paletted frame by label)
+        HIP_TRY(launch_palettize(g->n, a.nc, batch, llr, w->codes, w->palette, w->pal_ok, dg->col_orig, stream));
     {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order).
         // It only schedules — results never depend on it — so a shape it cannot
         // run (LDS beyond the device limit) decodes in index order instead.
@@ -1385,6 +1400,65 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     return QLDPC_OK;
 }
 
+// QKD_LDPC's (plan == NULL) or QKD_LDPC_RATE_ADAPT's per-trial window for
+// `batch` device-resident trials on `stream` (the current device is dg's):
+// frame build, decode, key comparison.  V2 decoders read the frame builder's
+// palette codes, so the f64 LLRs are written only into a caller workspace
+// (d_llr_ws, nullable); the other decoders read llr[] from it or, when it is
+// NULL, from the stream workspace's.
+int qkd_ldpc_window(qldpc_graph *g, DeviceGraph *dg, const qldpc_rate_plan *plan, const qldpc_params *p, int batch,
+                    const uint8_t *d_alice, const uint8_t *d_bob, const uint8_t *d_punct_alice,
+                    const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext, double *d_llr_ws,
+                    uint8_t *d_synd_ws, uint8_t *d_bits_out, uint32_t *d_iters_out, uint8_t *d_synd_ok_out,
+                    uint8_t *d_keys_match_out, hipStream_t s, uint64_t *frame_clk = nullptr) {
+    if (batch == 0) return QLDPC_OK;
+    const qldpc_rate_plan::Dev *pd = nullptr;
+    if (plan) {
+        for (auto &d : plan->devs)
+            if (d.device == dg->device) pd = &d;
+        if (!pd) return fail(QLDPC_EINVAL, "rate plan does not live on that device");
+    }
+    const bool v2 = g->variant == VAR_V2;
+    uint8_t *codes = nullptr, *pal_ok = nullptr;
+    double *palette = nullptr;
+    double *llr = d_llr_ws;
+    {
+        std::lock_guard<std::mutex> lk(dg->mu);
+        Workspace *w = workspace(dg, s);
+        if (v2) {
+            // the frame builder writes the V2 palette + codes straight into the
+            // stream's workspace, so the decoder skips the palettize pass
+            int r = ensure_codes(g, w, batch, s);
+            if (r) return r;
+            codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
+        } else if (!llr) {
+            if ((size_t)batch > w->llr_ws_frames) {
+                HIP_TRY(hipStreamSynchronize(s));
+                (void)hipFree(w->llr_ws);
+                w->llr_ws = nullptr;
+                w->llr_ws_frames = 0;
+                HIP_TRY(hipMalloc(&w->llr_ws, (size_t)batch * g->n * sizeof(double)));
+                w->llr_ws_frames = (size_t)batch;
+            }
+            llr = w->llr_ws;
+        }
+    }
+    if (plan)
+        HIP_TRY(launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
+                                       d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, llr,
+                                       d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
+    else
+        HIP_TRY(launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob, d_log_p,
+                                    llr, d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
+    int r = decode_on(g, dg, p, batch, llr, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s, v2,
+                      frame_clk);
+    if (r) return r;
+    // keys_match = arrays_equal(alice[_extended], bob_solution) (:1087, :1216)
+    if (d_keys_match_out)
+        HIP_TRY(launch_keys_match(batch, g->n, plan ? d_alice_ext : d_alice, d_bits_out, d_keys_match_out, s));
+    return QLDPC_OK;
+}
+
 template <typename T>
 int grow(T **p, size_t count) {
     if (*p) HIP_TRY(hipFree(*p));
@@ -1400,6 +1474,14 @@ extern "C" {
 const char *qldpc_last_error(void) { return g_last_error.c_str(); }
 
 const char *qldpc_version(void) { return "qkd_ldpc_v_amd 0.1.0 (gfx950)"; }
+
+int qldpc_device_count(int32_t *count) {
+    if (!count) return fail(QLDPC_EINVAL, "count is NULL");
+    int c = 0;
+    HIP_TRY(hipGetDeviceCount(&c));
+    *count = c;
+    return QLDPC_OK;
+}
 
 double qldpc_log_p(double qber) { return std::log((1. - qber) / qber); }
 
@@ -1463,6 +1545,16 @@ int qldpc_graph_create_on(int32_t n, int32_t m, const int32_t *row_ptr, const in
     return build_graph(n, m, row_ptr, col_idx, 0, out, false, &list);
 }
 
+int qldpc_graph_create_checked_on(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
+                                  const int32_t *col_ptr, const int32_t *row_idx, const int32_t *devices,
+                                  int32_t ndevices, qldpc_graph **out) {
+    if (!row_ptr || !col_idx || !col_ptr || !row_idx) return fail(QLDPC_EINVAL, "NULL adjacency array");
+    if (n <= 0 || m < 0) return fail(QLDPC_EINVAL, "invalid graph dimensions");
+    if (!devices || ndevices <= 0 || ndevices > 64) return fail(QLDPC_EINVAL, "need 1..64 devices");
+    const std::vector<int> list(devices, devices + ndevices);
+    return build_graph(n, m, row_ptr, col_idx, 0, out, false, &list, col_ptr, row_idx);
+}
+
 int qldpc_graph_create_host(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col_idx,
                             qldpc_graph **out) {
     return build_graph(n, m, row_ptr, col_idx, 0, out, true);
@@ -1523,11 +1615,21 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(kv.second.palette);
             (void)hipFree(kv.second.pal_ok);
             (void)hipFree(kv.second.split_ctl);
-            (void)hipFree(kv.second.llr_lab);
+            (void)hipFree(kv.second.llr_ws);
             if (kv.second.ev0) (void)hipEventDestroy(kv.second.ev0);
             if (kv.second.ev1) (void)hipEventDestroy(kv.second.ev1);
             (void)hipFree(kv.second.gtotal);
             (void)hipFree(kv.second.gstage);
+        }
+        for (auto &t : d->tslot) {
+            (void)hipFree(t.seeds); (void)hipFree(t.clk); (void)hipFree(t.alice); (void)hipFree(t.bob);
+            (void)hipFree(t.palice); (void)hipFree(t.pbob); (void)hipFree(t.alice_ext); (void)hipFree(t.synd);
+            (void)hipFree(t.bits); (void)hipFree(t.ok); (void)hipFree(t.km); (void)hipFree(t.iters);
+            (void)hipFree(t.tscratch); (void)hipFree(t.logp);
+            (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
+            if (t.ev0) (void)hipEventDestroy(t.ev0);
+            if (t.ev1) (void)hipEventDestroy(t.ev1);
+            if (t.stream) (void)hipStreamDestroy(t.stream);
         }
         HostIO &io = d->io;
         (void)hipFree(io.llr); (void)hipFree(io.post); (void)hipFree(io.synd); (void)hipFree(io.bits); (void)hipFree(io.ok); (void)hipFree(io.iters);
@@ -1768,8 +1870,7 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
     int rc = check_params(p);
     if (rc) return rc;
     if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
-    if (batch > 0 && (!d_alice || !d_bob || !d_log_p || !d_llr_ws || !d_synd_ws || !d_bits_out || !d_iters_out ||
-                      !d_synd_ok_out))
+    if (batch > 0 && (!d_alice || !d_bob || !d_log_p || !d_synd_ws || !d_bits_out || !d_iters_out || !d_synd_ok_out))
         return fail(QLDPC_EINVAL, "NULL device buffer");
     DeviceGraph *dg = find_dev(g, device);
     if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
@@ -1777,28 +1878,8 @@ int qldpc_qkd_ldpc_batch_device(qldpc_graph *g, int32_t device, const qldpc_para
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
-    const hipStream_t s = (hipStream_t)stream;
-    auto body = [&]() -> int {
-        // The frame builder writes the V2 palette + codes straight into the
-        // stream's workspace, so the decoder skips the palettize pass.
-        uint8_t *codes = nullptr, *pal_ok = nullptr;
-        double *palette = nullptr;
-        if (g->variant == VAR_V2) {
-            std::lock_guard<std::mutex> lk(dg->mu);
-            Workspace *w = workspace(dg, s);
-            int r = ensure_codes(g, w, batch, s);
-            if (r) return r;
-            codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
-        }
-        HIP_TRY(launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob, d_log_p,
-                                    d_llr_ws, d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
-        int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
-                          g->variant == VAR_V2);
-        if (r) return r;
-        if (d_keys_match_out) HIP_TRY(launch_keys_match(batch, g->n, d_alice, d_bits_out, d_keys_match_out, s));
-        return QLDPC_OK;
-    };
-    rc = body();
+    rc = qkd_ldpc_window(g, dg, nullptr, p, batch, d_alice, d_bob, nullptr, nullptr, d_log_p, nullptr, d_llr_ws,
+                         d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, d_keys_match_out, (hipStream_t)stream);
     (void)hipSetDevice(prev);
     return rc;
 }
@@ -2049,39 +2130,17 @@ int qldpc_qkd_ldpc_rate_adapt_batch_device(qldpc_graph *g, const qldpc_rate_plan
     if (rc) return rc;
     if (batch < 0) return fail(QLDPC_EINVAL, "batch must be >= 0");
     if (batch == 0) return QLDPC_OK;
-    if (!d_alice || !d_bob || !d_log_p || !d_alice_ext || !d_llr_ws || !d_synd_ws || !d_bits_out || !d_iters_out ||
+    if (!d_alice || !d_bob || !d_log_p || !d_alice_ext || !d_synd_ws || !d_bits_out || !d_iters_out ||
         !d_synd_ok_out || (plan->n_punct && (!d_punct_alice || !d_punct_bob)))
         return fail(QLDPC_EINVAL, "NULL device buffer");
     DeviceGraph *dg = find_dev(g, device);
-    const qldpc_rate_plan::Dev *pd = nullptr;
-    for (auto &d : plan->devs)
-        if (d.device == device) pd = &d;
-    if (!dg || !pd) return fail(QLDPC_EINVAL, "graph / plan does not live on that device");
+    if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
-    const hipStream_t s = (hipStream_t)stream;
-    auto body = [&]() -> int {
-        uint8_t *codes = nullptr, *pal_ok = nullptr;
-        double *palette = nullptr;
-        if (g->variant == VAR_V2) {
-            std::lock_guard<std::mutex> lk(dg->mu);
-            Workspace *w = workspace(dg, s);
-            int r = ensure_codes(g, w, batch, s);
-            if (r) return r;
-            codes = w->codes; palette = w->palette; pal_ok = w->pal_ok;
-        }
-        HIP_TRY(launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
-                                       d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, d_llr_ws,
-                                       d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
-        int r = decode_on(g, dg, p, batch, d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s,
-                          g->variant == VAR_V2);
-        if (r) return r;
-        // keys_match = arrays_equal(alice_extended, bob_solution) (:1216)
-        if (d_keys_match_out) HIP_TRY(launch_keys_match(batch, g->n, d_alice_ext, d_bits_out, d_keys_match_out, s));
-        return QLDPC_OK;
-    };
-    rc = body();
+    rc = qkd_ldpc_window(g, dg, plan, p, batch, d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext,
+                         d_llr_ws, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, d_keys_match_out,
+                         (hipStream_t)stream);
     (void)hipSetDevice(prev);
     return rc;
 }
@@ -2178,6 +2237,161 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
         (void)hipFree(scratch);
     }
     if (e != hipSuccess) return hip_fail(e, "trials");
+    return QLDPC_OK;
+}
+
+
+// ---- the batch seam of the simulation loop (src/simulation.cpp:721-746) ------
+int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber, int32_t count,
+                     const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out, uint8_t *synd_ok_out,
+                     uint8_t *keys_match_out, double *runtime_us_out, double *accurate_qber_out) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    int rc = check_params(p);
+    if (rc) return rc;
+    if (count < 0) return fail(QLDPC_EINVAL, "count must be >= 0");
+    if (g->devs.empty()) return fail(QLDPC_EINVAL, "graph has no device (host-only)");
+    const int n = g->n;
+    const uint64_t n_err = (uint64_t)((double)n * qber);
+    if (n_err == 0)  // run_trial's own check (src/simulation.cpp:552-553)
+        return fail(QLDPC_EINVAL, "Key size '" + std::to_string(n) + "' is too small for QBER.");
+    if (n_err > (uint64_t)n) return fail(QLDPC_EINVAL, "QBER must be <= 1");
+    const double q_acc = (double)n_err / (double)n;  // inject_errors' return (:922-933)
+    if (accurate_qber_out) *accurate_qber_out = q_acc;
+    if (count == 0) return QLDPC_OK;
+    if (!seeds || !iters_out || !synd_ok_out || !keys_match_out) return fail(QLDPC_EINVAL, "NULL host buffer");
+    if (plan && plan->n_punct + plan->n_short > n) return fail(QLDPC_EINVAL, "rate plan does not fit the graph");
+    const double lp = qldpc_log_p(q_acc);  // log((1 - q) / q) by the host C library (:1043)
+    const int n_punct = plan ? plan->n_punct : 0;
+    // Frames per chunk: the slot's own buffers within ~512 MiB (QLDPC_TRIAL_CHUNK overrides).
+    const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 + (n > 65536 ? 4 * (size_t)n : 0);
+    int cap = (int)std::max<size_t>(1, std::min<size_t>(16384, ((size_t)512 << 20) / per_frame));
+    if (env_int("QLDPC_TRIAL_CHUNK", 0) > 0) cap = env_int("QLDPC_TRIAL_CHUNK", 0);
+    const int G = (int)g->devs.size();
+    const int per = (count + G - 1) / G;
+    std::vector<int> rcs(G, QLDPC_OK);
+    std::vector<std::string> errs(G);
+    auto work = [&](int gi) {
+        DeviceGraph *dg = g->devs[gi].get();
+        const int lo = std::min(count, gi * per), hi = std::min(count, lo + per);
+        if (hi <= lo) return;
+        auto body = [&]() -> int {
+            HIP_TRY(hipSetDevice(dg->device));
+            std::lock_guard<std::mutex> lk(dg->trial_mu);
+            const std::vector<double> lpv((size_t)std::min(cap, hi - lo), lp);
+            // results of a slot's chunk: wait for it, then each trial's share of
+            // the chunk's window (QKD_LDPC's per-trial window on device, HIP
+            // events on its stream) in proportion to its own decode span
+            auto harvest = [&](TrialSlot &t) -> int {
+                if (t.nb == 0) return QLDPC_OK;
+                const int nb = t.nb;
+                t.nb = 0;
+                HIP_TRY(hipStreamSynchronize(t.stream));
+                int r = split_check(g, dg, t.stream);
+                if (r) return r;
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, t.ev0, t.ev1));
+                double span_sum = 0.;
+                for (int i = 0; i < nb; ++i) span_sum += (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
+                for (int i = 0; i < nb; ++i) {
+                    iters_out[t.f0 + i] = t.h_iters[i];
+                    synd_ok_out[t.f0 + i] = t.h_ok[i];
+                    keys_match_out[t.f0 + i] = t.h_km[i];
+                    if (runtime_us_out) {
+                        const double span = (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
+                        runtime_us_out[t.f0 + i] =
+                            span_sum > 0. ? 1e3 * (double)ms * span / span_sum : 1e3 * (double)ms / nb;
+                    }
+                }
+                return QLDPC_OK;
+            };
+            auto ensure = [&](TrialSlot &t, int nb) -> int {
+                if (!t.stream) HIP_TRY(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
+                if (!t.ev0) HIP_TRY(hipEventCreate(&t.ev0));
+                if (!t.ev1) HIP_TRY(hipEventCreate(&t.ev1));
+                if ((size_t)nb > t.cap || (size_t)std::max(n_punct, 1) > t.cap_punct) {
+                    const size_t c = std::max((size_t)nb, t.cap), cp = std::max((size_t)std::max(n_punct, 1), t.cap_punct);
+                    int r;
+                    if ((r = grow(&t.seeds, c)) || (r = grow(&t.clk, 2 * c)) || (r = grow(&t.alice, c * n)) ||
+                        (r = grow(&t.bob, c * n)) || (r = grow(&t.alice_ext, c * n)) || (r = grow(&t.bits, c * n)) ||
+                        (r = grow(&t.synd, c * (size_t)std::max(g->m, 1))) || (r = grow(&t.ok, c)) ||
+                        (r = grow(&t.km, c)) || (r = grow(&t.iters, c)) || (r = grow(&t.logp, c)) ||
+                        (r = grow(&t.palice, c * cp)) || (r = grow(&t.pbob, c * cp)))
+                        return r;
+                    const size_t sw = trials_scratch_words(n, (int)c);
+                    if (sw && (r = grow(&t.tscratch, sw))) return r;
+                    (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
+                    t.h_iters = nullptr; t.h_ok = nullptr; t.h_km = nullptr; t.h_clk = nullptr; t.cap = 0;
+                    HIP_TRY(hipHostMalloc(&t.h_iters, c * sizeof(uint32_t)));
+                    HIP_TRY(hipHostMalloc(&t.h_ok, c));
+                    HIP_TRY(hipHostMalloc(&t.h_km, c));
+                    HIP_TRY(hipHostMalloc(&t.h_clk, 2 * c * sizeof(uint64_t)));
+                    t.cap = c;
+                    t.cap_punct = cp;
+                }
+                return QLDPC_OK;
+            };
+            int r = QLDPC_OK;
+            int c = 0;
+            for (int f = lo; f < hi && !r; ++c) {
+                TrialSlot &t = dg->tslot[c & 1];
+                if ((r = harvest(t))) break;
+                const int nb = std::min(cap, hi - f);
+                if ((r = ensure(t, nb))) break;
+                auto enqueue = [&]() -> int {
+                    HIP_TRY(hipMemcpyAsync(t.seeds, seeds + f, (size_t)nb * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                           t.stream));
+                    HIP_TRY(hipMemcpyAsync(t.logp, lpv.data(), (size_t)nb * sizeof(double), hipMemcpyHostToDevice,
+                                           t.stream));
+                    // run_trial's keys (+ QKD_LDPC_RATE_ADAPT's punctured draws), seed = seeds[n] + curr_sim (:743)
+                    HIP_TRY(launch_trials(n, n_err, nb, t.seeds, seed_add, t.alice, t.bob, t.tscratch, n_punct,
+                                          t.palice, t.pbob, t.stream));
+                    HIP_TRY(hipEventRecord(t.ev0, t.stream));
+                    int rr = qkd_ldpc_window(g, dg, plan, p, nb, t.alice, t.bob, t.palice, t.pbob, t.logp, t.alice_ext,
+                                             nullptr, t.synd, t.bits, t.iters, t.ok, t.km, t.stream, t.clk);
+                    if (rr) return rr;
+                    HIP_TRY(hipEventRecord(t.ev1, t.stream));
+                    HIP_TRY(hipMemcpyAsync(t.h_iters, t.iters, (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                           t.stream));
+                    HIP_TRY(hipMemcpyAsync(t.h_ok, t.ok, (size_t)nb, hipMemcpyDeviceToHost, t.stream));
+                    HIP_TRY(hipMemcpyAsync(t.h_km, t.km, (size_t)nb, hipMemcpyDeviceToHost, t.stream));
+                    HIP_TRY(hipMemcpyAsync(t.h_clk, t.clk, 2 * (size_t)nb * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                           t.stream));
+                    return QLDPC_OK;
+                };
+                if ((r = enqueue())) {
+                    (void)hipStreamSynchronize(t.stream);  // nothing of this call stays in flight
+                    break;
+                }
+                t.f0 = f;
+                t.nb = nb;
+                f += nb;
+            }
+            for (auto &t : dg->tslot) {
+                if (r) {  // an error: drain what is in flight, keep the first error
+                    if (t.nb) (void)hipStreamSynchronize(t.stream);
+                    t.nb = 0;
+                } else {
+                    r = harvest(t);
+                }
+            }
+            return r;
+        };
+        const int r = body();
+        rcs[gi] = r;
+        if (r) errs[gi] = g_last_error;
+    };
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    if (G == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int gi = 0; gi < G; ++gi) th.emplace_back(work, gi);
+        for (auto &t : th) t.join();
+    }
+    (void)hipSetDevice(prev);
+    for (int gi = 0; gi < G; ++gi)
+        if (rcs[gi]) return fail(rcs[gi], errs[gi]);
     return QLDPC_OK;
 }
 

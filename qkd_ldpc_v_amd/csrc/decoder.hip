@@ -102,6 +102,8 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
         STAMP(ST_SETUP_WAIT);
         const int f = __builtin_amdgcn_readfirstlane(*s_frame);  // wave-uniform: SGPR addressing
         if (f >= a.batch) break;
+        uint64_t clk0 = 0;  // the trial's own span inside the batch (a.frame_clk)
+        if (tid == 0 && a.frame_clk) clk0 = __builtin_amdgcn_s_memrealtime();
         const double *llr = a.llr + (size_t)f * n;
         const uint8_t *sy = a.synd + (size_t)f * m;
         for (int j = tid; j < m; j += T) rowflag[j] = sy[j] & 1;
@@ -309,6 +311,10 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
         if (tid == 0) {
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
+            if (a.frame_clk) {
+                a.frame_clk[2 * (size_t)f] = clk0;
+                a.frame_clk[2 * (size_t)f + 1] = __builtin_amdgcn_s_memrealtime();
+            }
         }
         STAMP(ST_OUT);
         __syncthreads();

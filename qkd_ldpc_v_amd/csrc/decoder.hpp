@@ -149,9 +149,19 @@ struct DecodeArgs {
     // Bank-aware bit labels (relabel.cpp; one-workgroup register shapes): the
     // graph's metadata and the frame codes use labels, llr / bits / posterior
     // the reference's bit ids.  nullptr: identity.
-    const int32_t *col_orig;        // [n] label -> bit id (the frame codes and llr[] the kernel reads are in labels)
+    const int32_t *col_orig;        // [n] label -> bit id (the frame codes the kernel reads are in labels)
     const int32_t *col_lab;         // [n] bit id -> label (outputs: bits / posterior in bit ids)
+    // ... a frame the palette cannot hold is copied into label order at frame
+    // setup, into its workgroup's scratch at this offset (doubles); -1: none
+    long long llr_lab_wg_offset;
+    // Per-frame decode span (nullable): [batch][2] s_memrealtime ticks (100 MHz)
+    // at the frame's claim and at its results — the trial's own time inside the
+    // batch (the reference times each trial's QKD_LDPC call, src/simulation.cpp:559-568)
+    uint64_t *frame_clk;
 };
+
+// Frequency of s_memrealtime (gfx9: a constant 100 MHz clock).
+constexpr double FRAME_CLK_HZ = 100.0e6;
 
 // The persistent decoders' frame claim: the next frame of the launch's claim
 // order (order.hip; results never depend on it).  >= batch: none left.
@@ -186,7 +196,7 @@ constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per la
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, const int32_t *col_orig, double *llr_lab, hipStream_t stream);
+                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
 size_t trials_lds_bytes(int n);
 size_t trials_scratch_words(int n, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,

@@ -360,6 +360,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // instead of VGPRs with waterfall loops around each access
         const int f = __builtin_amdgcn_readfirstlane(*s_frame);
         if (f >= a.batch) break;
+        // the trial's own span inside the batch starts at its claim (a.frame_clk)
+        uint64_t clk0 = 0;
+        if (tid == 0 && a.frame_clk) clk0 = __builtin_amdgcn_s_memrealtime();
         // SPLIT: this part's lanes, waves, metadata and rows; the group barrier
         const int rank = SPLIT ? __builtin_amdgcn_readfirstlane(s_part[0]) : 0;
         const int tg = SPLIT ? rank * REG_TSTRIDE + tid : tid;
@@ -414,9 +417,17 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         const bool paletted = a.pal_ok[f] != 0;
         // Non-paletted frames gather llr[] through a buffer resource: a distinct
         // load kind the compiler cannot fuse with the LDS palette read into a
-        // flat load.
-        const __amdgpu_buffer_rsrc_t llr_rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(a.llr + (size_t)f * n), (short)0, paletted ? 0 : n * 8, 0x00020000);
+        // flat load.  Relabelled graphs read it by label: such a frame is first
+        // copied into label order in this workgroup's scratch (the setup
+        // barrier below orders the copy before every read).
+        const double *llr_f = a.llr + (size_t)f * n;
+        if (!paletted && a.llr_lab_wg_offset >= 0) {
+            double *dst = a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles + a.llr_lab_wg_offset;
+            for (int i = tid; i < n; i += T) dst[i] = llr_f[a.col_orig[i]];
+            llr_f = dst;
+        }
+        const __amdgpu_buffer_rsrc_t llr_rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)llr_f, (short)0, paletted ? 0 : n * 8, 0x00020000);
         const uint8_t *gcodes = a.codes + (size_t)f * nc;
         if constexpr (SPLIT) {
             if (tid < 4) pal[tid] = a.palette[(size_t)f * 4 + tid];
@@ -453,7 +464,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 if (paletted) return pal[codes[col]];
             }
-            // (relabelled graphs: decode_on hands over llr[] in label order)
+            // (relabelled graphs: llr_rs holds the frame's label-order copy)
             return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(llr_rs, col * 8, 0, 0));
         };
         // total starts as the channel LLRs: the check-node scan of iteration 0
@@ -1215,6 +1226,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         if (tid == 0 && rank == 0) {
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
+            if (a.frame_clk) {
+                a.frame_clk[2 * (size_t)f] = clk0;
+                a.frame_clk[2 * (size_t)f + 1] = __builtin_amdgcn_s_memrealtime();
+            }
         }
         STAMP(ST_OUT);
         __syncthreads();
@@ -1234,8 +1249,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 // with more gets pal_ok = 0 and the decoder gathers its llr[] instead.  Unused
 // entries repeat entry 0 (the SPA iteration-0 test reads all four).
 __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const double *llr, uint8_t *codes,
-                                                        double *palette, uint8_t *pal_ok, const int32_t *col_orig,
-                                                        double *llr_lab) {
+                                                        double *palette, uint8_t *pal_ok, const int32_t *col_orig) {
     __shared__ unsigned long long pv[4];
     __shared__ int pcount, over;
     const size_t f = blockIdx.x;
@@ -1279,8 +1293,6 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
                 const unsigned long long x = v[col_orig ? col_orig[i] : i];
                 for (int q = 1; q < 4; ++q)
                     if (q < cnt && x == pv[q]) code = q;
-                // a frame the palette cannot hold is decoded from llr[]: in label order
-                if (llr_lab && over) llr_lab[f * (size_t)n + i] = __builtin_bit_cast(double, x);
             }
             byte |= code << (2 * s);
         }
@@ -1388,10 +1400,10 @@ hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_b
 }
 
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
-                            uint8_t *pal_ok, const int32_t *col_orig, double *llr_lab, hipStream_t stream) {
+                            uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     hipLaunchKernelGGL(palettize_kernel, dim3(batch), dim3(256), 0, stream, n, nc, llr, codes, palette, pal_ok,
-                       col_orig, llr_lab);
+                       col_orig);
     return hipGetLastError();
 }
 

@@ -91,6 +91,15 @@ class DecodeOutput:
     posterior: np.ndarray | None  # float64[batch, n] total_bit_llr
 
 
+@dataclass
+class TrialsOutput:
+    iterations: np.ndarray  # uint32[count] decoding_result.iterations_num
+    synd_ok: np.ndarray     # uint8[count]  decoding_result.syndromes_match
+    keys_match: np.ndarray  # uint8[count]  LDPC_result.keys_match
+    runtime_us: np.ndarray  # float64[count] trial_result.runtime (share of the chunk window, see the C ABI)
+    accurate_qber: float    # trial_result.accurate_QBER (the same for every trial)
+
+
 def _canonical_adjacency(H: HMatrix) -> bool:
     """check_nodes rows ascending and bit_nodes their ascending transpose: the
     reference's slot pairing is then the edge itself (src/qkd_ldpc_algorithm.cpp:
@@ -118,18 +127,20 @@ class Graph:
         self.H = H
         self.n, self.m = H.n, H.m
         g = ctypes.c_void_p()
-        if (host_only or devices is not None) and not _canonical_adjacency(H):
-            # (these entries take check_nodes only and assume bit_nodes is their
-            # ascending transpose; the reference's occurrence pairing of other
-            # lists needs qldpc_graph_create_checked)
-            raise ValueError("unsorted adjacency: use Graph(H) / Graph(H, device_mask=...)")
+        self.host_only = bool(host_only)
+        if host_only and not _canonical_adjacency(H):
+            # (the host-only planner takes check_nodes only and assumes bit_nodes
+            # is their ascending transpose; the reference's occurrence pairing of
+            # other lists needs qldpc_graph_create_checked)
+            raise ValueError("unsorted adjacency: use Graph(H) / Graph(H, devices=...)")
         if host_only:
             check(lib().qldpc_graph_create_host(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ctypes.byref(g)),
                   "qldpc_graph_create_host")
         elif devices is not None:
             dl = np.ascontiguousarray(devices, np.int32)
-            check(lib().qldpc_graph_create_on(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(dl), int(dl.size),
-                                              ctypes.byref(g)), "qldpc_graph_create_on")
+            check(lib().qldpc_graph_create_checked_on(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(H.col_ptr),
+                                                      ptr(H.row_idx), ptr(dl), int(dl.size), ctypes.byref(g)),
+                  "qldpc_graph_create_checked_on")
         else:
             check(lib().qldpc_graph_create_checked(H.n, H.m, ptr(H.row_ptr), ptr(H.col_idx), ptr(H.col_ptr),
                                                    ptr(H.row_idx), int(device_mask), ctypes.byref(g)),
@@ -166,11 +177,14 @@ class Graph:
         return {"n": n.value, "m": m.value, "nnz": nnz.value, "devices": nd.value}
 
     def plan(self, device: int = 0, algorithm: int = 0) -> dict:
+        """Launch geometry; a host-only graph has no device, so workgroups is None."""
         lanes, epl, wgs, lds = (ctypes.c_int32() for _ in range(4))
         var = ctypes.c_char_p()
         check(lib().qldpc_graph_plan(self._g, device, algorithm, ctypes.byref(lanes), ctypes.byref(epl),
-                                     ctypes.byref(wgs), ctypes.byref(lds), ctypes.byref(var)), "qldpc_graph_plan")
-        return {"lanes": lanes.value, "edges_per_lane": epl.value, "workgroups": wgs.value,
+                                     None if self.host_only else ctypes.byref(wgs), ctypes.byref(lds),
+                                     ctypes.byref(var)), "qldpc_graph_plan")
+        return {"lanes": lanes.value, "edges_per_lane": epl.value,
+                "workgroups": None if self.host_only else wgs.value,
                 "lds_bytes": lds.value, "variant": var.value.decode()}
 
     def set_kernel_timing(self, enabled: bool = True) -> None:
@@ -242,6 +256,24 @@ class Graph:
             _dp(llr_ws), _dp(synd_ws), _dp(bits), _dp(iters), _dp(ok),
             _dp(keys_match), _stream_ptr(stream, dev)), "qldpc_qkd_ldpc_batch_device")
 
+
+    # ---- the simulation loop's batch seam (host pointers; shards over the devices) ----
+    def run_trials(self, params: Params, qber: float, seeds, seed_add: int = 0, plan: "RatePlan | None" = None):
+        """run_trial for every seed (src/simulation.cpp:540-576; seed = seeds[t] +
+        seed_add) on device through qldpc_run_trials.  -> TrialsOutput."""
+        sd = np.ascontiguousarray(seeds, np.uint64)
+        cnt = int(sd.size)
+        it = np.empty(cnt, np.uint32)
+        ok = np.empty(cnt, np.uint8)
+        km = np.empty(cnt, np.uint8)
+        rt = np.empty(cnt, np.float64)
+        q = ctypes.c_double(0.0)
+        p = params.c()
+        check(lib().qldpc_run_trials(self._g, None if plan is None else plan.handle, ctypes.byref(p), float(qber),
+                                     cnt, sd.ctypes.data, int(seed_add) & 0xFFFFFFFFFFFFFFFF, it.ctypes.data,
+                                     ok.ctypes.data, km.ctypes.data, rt.ctypes.data, ctypes.byref(q)),
+              "qldpc_run_trials")
+        return TrialsOutput(it, ok, km, rt, q.value)
 
     def rate_plan(self, punctured, shortened) -> "RatePlan":
         return RatePlan(self, punctured, shortened)

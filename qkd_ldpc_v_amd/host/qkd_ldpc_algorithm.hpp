@@ -41,6 +41,7 @@ struct config_data {
     bool ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD{};
     double DECODING_ALG_MSG_LLR_THRESHOLD{};
     bool ENABLE_PRIVACY_MAINTENANCE{};
+    bool ENABLE_CODE_RATE_ADAPTATION{};
 };
 inline config_data CFG;
 
@@ -201,7 +202,7 @@ inline std::vector<decoding_result> decode_batch(const H_matrix &matrix, const s
                                                  const std::vector<uint8_t> &syndrome, size_t batch,
                                                  const decoding_scaling_factors &sf,
                                                  std::vector<uint8_t> &bits_out) {
-    auto g = impl::graph_cache().get(matrix);
+    auto e = impl::graph_cache().get(matrix);
     const size_t n = matrix.bit_nodes.size(), m = matrix.check_nodes.size();
     if (llr.size() < batch * n || syndrome.size() < batch * m)
         throw std::runtime_error("decode_batch: llr / syndrome shorter than batch frames");
@@ -211,12 +212,36 @@ inline std::vector<decoding_result> decode_batch(const H_matrix &matrix, const s
     qldpc_params p{(int32_t)CFG.DECODING_ALGORITHM, (int32_t)CFG.DECODING_ALG_MAX_ITERATIONS,
                    CFG.ENABLE_DECODING_ALG_MSG_LLR_THRESHOLD ? 1 : 0, 0, CFG.DECODING_ALG_MSG_LLR_THRESHOLD,
                    sf.primary, sf.secondary};
-    if (qldpc_decode_batch(g.get(), &p, (int32_t)batch, llr.data(), syndrome.data(), bits_out.data(), it.data(),
+    if (qldpc_decode_batch(e->g.get(), &p, (int32_t)batch, llr.data(), syndrome.data(), bits_out.data(), it.data(),
                            ok.data(), nullptr))
         impl::raise("qldpc_decode_batch");
     std::vector<decoding_result> res(batch);
     for (size_t f = 0; f < batch; ++f) res[f] = {it[f], ok[f] != 0};
     return res;
+}
+
+// The simulation loop's batch seam: run_trial for every seed of one
+// combination (src/simulation.cpp:540-576, 721-746; trial t seeded with
+// seeds[t] + seed_add), on the GPUs the cached graph lives on.  With
+// CFG.ENABLE_CODE_RATE_ADAPTATION the trials run QKD_LDPC_RATE_ADAPT with
+// matrix_params' punctured / shortened positions, else QKD_LDPC.
+struct trial_result {  // src/simulation.hpp:36-41 (runtime in microseconds, as a double)
+    LDPC_result ldpc_res{};
+    double accurate_QBER{};
+    double runtime_us{};
+};
+inline std::vector<trial_result> run_trials(const H_matrix &matrix, double QBER, const std::vector<size_t> &seeds,
+                                            size_t seed_add, const H_matrix_params &matrix_params = {},
+                                            const decoding_scaling_factors &sf = {}) {
+    const bool ra = CFG.ENABLE_CODE_RATE_ADAPTATION;
+    double q = 0.;
+    const auto r = impl::run_trials(matrix, QBER, seeds, seed_add, sf.primary, sf.secondary, detail::cfg(),
+                                    ra ? &matrix_params.punctured_bits : nullptr,
+                                    ra ? &matrix_params.shortened_bits : nullptr, &q);
+    std::vector<trial_result> out(r.size());
+    for (size_t t = 0; t < r.size(); ++t) out[t] = {{{r[t].iterations_num, r[t].syndromes_match}, r[t].keys_match}, q,
+                                                    r[t].runtime_us};
+    return out;
 }
 
 // Device graphs are cached by H content; free one (or all) explicitly.

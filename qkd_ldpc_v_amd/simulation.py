@@ -16,7 +16,9 @@ the command line (the reference derives it from matrix_format under its source
 tree) and its *.mtrx files are taken in name order (the reference uses
 directory order, which the filesystem decides); the untainted-puncturing
 search for a missing .untp file runs and writes the file, as the reference's;
-throughput columns report the GPU pipeline's amortised per-trial time.
+the throughput columns' per-trial time is each trial's share of its GPU
+chunk's measured window, in proportion to its own decode span (the reference
+times each trial's QKD_LDPC call alone on one core; qldpc_run_trials).
 """
 from __future__ import annotations
 
@@ -31,7 +33,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import ALGORITHM_NAMES, Params, check, lib, log_p
+from ._lib import ALGORITHM_NAMES, Params, check, lib
 from .graph import Graph, adapt_code_rate, load_matrix, select_punctured_untainted, trial_seeds, xoshiro_state
 
 EPSILON = 1e-6  # src/config.hpp:199
@@ -408,127 +410,57 @@ def shard_ranges(total: int, shards: int) -> list[tuple[int, int]]:
     return [(min(total, k * per), min(total, (k + 1) * per)) for k in range(shards)]
 
 
-def _run_shard(cfg, H, c, sim, p, graph, plan, dev, stream, seeds, b, e, max_batch):
-    """Trials [b, e) of one combination on one device/stream: run_trial's keys
-    (device generator), then QKD_LDPC[_RATE_ADAPT]'s window (fused entry).
-    -> (iterations, syndromes_match, keys_match, accurate_qber, seconds in the window)."""
-    import torch
-
-    from .graph import trials_device, trials_rate_adapt_device
-
-    ra = c.punctured is not None
-    it_all, ok_all, km_all = [], [], []
-    t_pipe = 0.0
-    q_acc = None
-    with torch.cuda.device(dev), torch.cuda.stream(stream):
-        for b0 in range(b, e, max_batch):
-            nb = min(max_batch, e - b0)
-            ds = torch.from_numpy(seeds[b0:b0 + nb].view(np.int64)).to(dev)
-            ta = torch.empty((nb, H.n), dtype=torch.uint8, device=dev)
-            tb = torch.empty_like(ta)
-            np_ = max(1, c.punctured.size) if ra else 1
-            pa = torch.empty((nb, np_), dtype=torch.uint8, device=dev)
-            pb = torch.empty_like(pa)
-            # trial seed = seeds[n] + curr_sim (src/simulation.cpp:743)
-            if ra:
-                q_acc = trials_rate_adapt_device(H.n, c.config_qber, ds, c.punctured.size, ta, tb, pa, pb,
-                                                 seed_add=sim, stream=stream)
-            else:
-                q_acc = trials_device(H.n, c.config_qber, ds, ta, tb, seed_add=sim, stream=stream)
-            lp = torch.full((nb,), log_p(q_acc), dtype=torch.float64, device=dev)  # the C library's log (:1043)
-            llr = torch.empty((nb, H.n), dtype=torch.float64, device=dev)
-            syn = torch.empty((nb, H.m), dtype=torch.uint8, device=dev)
-            bits = torch.empty_like(ta)
-            it = torch.empty(nb, dtype=torch.int32, device=dev)
-            ok = torch.empty(nb, dtype=torch.uint8, device=dev)
-            km = torch.empty(nb, dtype=torch.uint8, device=dev)
-            stream.synchronize()
-            t0 = time.perf_counter()
-            if ra:
-                ax = torch.empty_like(ta)
-                graph.qkd_ldpc_rate_adapt_device(plan, p, ta, tb, pa, pb, lp, ax, llr, syn, bits, it, ok, km,
-                                                 stream=stream)
-            else:
-                graph.qkd_ldpc_device(p, ta, tb, lp, llr, syn, bits, it, ok, km, stream=stream)
-            stream.synchronize()
-            t_pipe += time.perf_counter() - t0
-            it_all.append(it.cpu().numpy())
-            ok_all.append(ok.cpu().numpy())
-            km_all.append(km.cpu().numpy())
-    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
-    return cat(it_all, np.int64), cat(ok_all, bool), cat(km_all, bool), q_acc, t_pipe
-
-
-def run(cfg: Config, mats, combos, device: int = 0, max_batch: int = 4096, log=print, devices=None):
+def run(cfg: Config, mats, combos, device: int = 0, log=print, devices=None):
     """The simulation loop over combinations (src/simulation.cpp:700-760).
 
-    devices: the GPUs to shard each combination's trials over (default
-    [device]).  The reference runs TRIALS_NUMBER trials of a combination on a
-    thread pool (:721,740-746); here the trial range is split in contiguous
-    slices, one per entry of `devices`, each decoded by its own host thread on
-    its own stream and graph replica, with no collective: the per-trial
-    results are concatenated in trial order on the host before the statistics
-    (process_trials_results, :580-690).  An entry may repeat a device (several
-    concurrent shards on one GPU).  The statistics do not depend on the
-    sharding: every trial's result is a function of its seed alone."""
-    import threading
-
-    import torch
-
+    Each combination's TRIALS_NUMBER trials go through the C ABI's batch seam
+    (qldpc_run_trials: the body of the reference's pool.detach_loop over
+    run_trial, :721-746): the per-trial seeds in, and per trial
+    {iterations_num, syndromes_match, keys_match, runtime} out; keys, frames,
+    decode and key comparison all stay on device.  devices: the GPUs the
+    trials are sharded over (default [device]) — contiguous slices, one host
+    thread and stream pair per entry inside the library, no collective.  An
+    entry may repeat a device (several concurrent shards on one GPU).  The
+    statistics do not depend on the sharding: every trial's result is a
+    function of its seed alone."""
     devs = [int(d) for d in (devices if devices else [device])]
-    torch.cuda.set_device(devs[0])
-    streams = [torch.cuda.Stream(torch.device("cuda", d)) for d in devs]
     seeds = trial_seeds(cfg.simulation_seed, cfg.trials_number)
-    graphs = {}  # (matrix, device) -> Graph replica
+    graphs = {}  # matrix -> Graph replicated on devs
     results = []
     for sim, c in enumerate(combos):
         path, H = mats[c.matrix_index]
         p = Params(cfg.decoding_algorithm, cfg.max_iterations, cfg.threshold_enabled, cfg.threshold, c.primary,
                    c.secondary)
-        ra = c.punctured is not None
-        gp = {}
-        for d in sorted(set(devs)):
-            key = (c.matrix_index, d)
-            if key not in graphs:
-                with torch.cuda.device(d):
-                    graphs[key] = Graph(H)
-            gp[d] = (graphs[key], graphs[key].rate_plan(c.punctured, c.shortened) if ra else None)
-        ranges = shard_ranges(cfg.trials_number, len(devs))
-        outs = [None] * len(devs)
-        errs = []
-
-        def work(k):
-            try:
-                d = devs[k]
-                g, plan = gp[d]
-                outs[k] = _run_shard(cfg, H, c, sim, p, g, plan, torch.device("cuda", d), streams[k], seeds,
-                                     ranges[k][0], ranges[k][1], max_batch)
-            except BaseException as e:  # reported after the join, like the C ABI's per-device errors
-                errs.append(e)
-
-        if len(devs) == 1:
-            work(0)
-        else:
-            th = [threading.Thread(target=work, args=(k,)) for k in range(len(devs))]
-            for t in th:
-                t.start()
-            for t in th:
-                t.join()
-        if errs:
-            raise errs[0]
-        it = np.concatenate([o[0] for o in outs])
-        ok = np.concatenate([o[1] for o in outs])
-        km = np.concatenate([o[2] for o in outs])
-        q_acc = next(o[3] for o in outs if o[3] is not None)
-        t_pipe = max(o[4] for o in outs)  # shards run concurrently
-        r = _stats(cfg, sim, os.path.basename(path), H, c, q_acc, it, ok, km, t_pipe)
+        if c.matrix_index not in graphs:
+            graphs[c.matrix_index] = Graph(H, devices=devs)
+        g = graphs[c.matrix_index]
+        plan = g.rate_plan(c.punctured, c.shortened) if c.punctured is not None else None
+        # trial seed = seeds[n] + curr_sim (:743)
+        out = g.run_trials(p, c.config_qber, seeds, seed_add=sim, plan=plan)
+        r = _stats(cfg, sim, os.path.basename(path), H, c, out.accurate_qber, out.iterations.astype(np.int64),
+                   out.synd_ok.astype(bool), out.keys_match.astype(bool), out.runtime_us)
         results.append(r)
         log(f"[{sim + 1}/{len(combos)}] {r['matrix_filename']} QBER={c.config_qber:.4f} "
             f"FER={1 - r['ratio_success_ldpc']:.4f} iters={r['iter_mean']:.2f}")
     return results
 
 
-def _stats(cfg, sim, fname, H, c, q_acc, it, ok, km, t_pipe) -> dict:
+def throughput_stats(out_len: int, runtime_us: np.ndarray, trials_number: int, rtt_ms: float | None = None):
+    """THROUGHPUT_MEAN / STD / MIN / MAX of process_trials_results
+    (src/simulation.cpp:626-681): per trial out_len / runtime in bits/s (plus
+    the RTT when CONSIDER_RTT), mean and population std over TRIALS_NUMBER, each
+    truncated to an integer as the reference's size_t fields.  runtime_us: the
+    trial_result::runtime of each trial (qldpc_run_trials: its share of its
+    chunk's measured window by its own decode span)."""
+    rt = np.asarray(runtime_us, np.float64)
+    denom = rt + (rtt_ms * 1000.0 if rtt_ms is not None else 0.0)
+    tp = out_len * 1e6 / denom
+    mean = float(tp.sum()) / trials_number
+    std = math.sqrt(float(((tp - mean) ** 2).sum()) / trials_number)
+    return int(mean), int(std), int(tp.min()), int(tp.max())
+
+
+def _stats(cfg, sim, fname, H, c, q_acc, it, ok, km, runtime_us) -> dict:
     """process_trials_results (src/simulation.cpp:580-690)."""
     succ = it[ok]
     mean = float(succ.mean()) if succ.size else 0.0
@@ -543,10 +475,8 @@ def _stats(cfg, sim, fname, H, c, q_acc, it, ok, km, t_pipe) -> dict:
          "adapted_rate": c.adapted_rate, "primary": c.primary, "secondary": c.secondary}
     if cfg.enable_throughput_measurement:
         out_len = H.n - c.bits_to_remove if (cfg.rate_adaptation or cfg.enable_privacy_maintenance) else H.n
-        per_trial_us = t_pipe * 1e6 / cfg.trials_number  # amortised over the GPU batch
-        denom = per_trial_us + (cfg.rtt * 1000.0 if cfg.consider_rtt else 0.0)
-        tp = out_len * 1e6 / denom
-        r.update(tp_mean=int(tp), tp_std=0, tp_min=int(tp), tp_max=int(tp))
+        tp = throughput_stats(out_len, runtime_us, cfg.trials_number, cfg.rtt if cfg.consider_rtt else None)
+        r.update(tp_mean=tp[0], tp_std=tp[1], tp_min=tp[2], tp_max=tp[3])
     return r
 
 

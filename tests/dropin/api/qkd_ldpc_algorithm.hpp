@@ -60,6 +60,8 @@ struct config_data {  // the members the decode path and run_trial read
     size_t SIMULATION_SEED{};
     bool ENABLE_PRIVACY_MAINTENANCE{};
     bool ENABLE_THROUGHPUT_MEASUREMENT{};
+    bool CONSIDER_RTT{};
+    double RTT{};
     size_t DECODING_ALGORITHM{};
     size_t DECODING_ALG_MAX_ITERATIONS{};
     size_t MATRIX_FORMAT{};

@@ -13,6 +13,13 @@
 //       alice, bob, q, sf, params, prng) when position lists are given
 //       (CFG.ENABLE_CODE_RATE_ADAPTATION), else QKD_LDPC(matrix, alice, bob, q,
 //       sf, params).  Prints "iterations syndromes_match keys_match" per trial.
+//   run_trial_check badsyndrome <matrix> <format>
+//       sum_product_decoding with a syndrome holding a 2 (no GPU needed: the
+//       drop-in refuses it before any device work) -> "ERROR: ..."
+//   run_trial_check keycost <matrix> <format> <reps>
+//       host cost of the graph cache's keys per decoder call (no GPU):
+//       "keycost_us fast <us> full <us>" — the O(1) key every call takes, the
+//       full content fingerprint a miss takes
 //   run_trial_check reuse  <matrixA> <fmtA> <matrixB> <fmtB> <alg> <primary> <secondary> <qber> <max_it> <seeds.txt>
 //       the reference's config-after-config loop: trials on A, then B loaded
 //       INTO THE SAME H_matrix object (same address, same n/m/nnz when B is a
@@ -28,59 +35,15 @@
 
 #include "qkd_ldpc_algorithm.hpp"  // tests/dropin/api: the reference's interface
 #include "qkd_ldpc_hip.h"
+#include "trial_common.hpp"
+#include "../../qkd_ldpc_v_amd/host/qkd_ldpc_impl.hpp"
+#include <chrono>
 
 config_data CFG;  // defined by the reference's src/config.cpp
 
 namespace {
 
-// fill_random_bits / inject_errors (src/array_and_matrix_operations.cpp:889-933).
-void fill_random_bits(XoshiroCpp::Xoshiro256PlusPlus &prng, std::vector<int> &bit_array) {
-    std::uniform_int_distribution<int> distribution(0, 1);
-    for (size_t i = 0; i < bit_array.size(); ++i) bit_array[i] = distribution(prng);
-}
-
-double inject_errors(XoshiroCpp::Xoshiro256PlusPlus &prng, const std::vector<int> &bit_array, double QBER,
-                     std::vector<int> &out) {
-    const size_t len = bit_array.size();
-    const size_t num_errors = static_cast<size_t>(static_cast<double>(len) * QBER);
-    out = bit_array;
-    if (num_errors > 0) {
-        std::vector<size_t> pos(len);
-        for (size_t i = 0; i < len; ++i) pos[i] = i;
-        std::shuffle(pos.begin(), pos.end(), prng);
-        for (size_t i = 0; i < num_errors; ++i) out[pos[i]] ^= 1;
-    }
-    return static_cast<double>(num_errors) / static_cast<double>(len);
-}
-
-void load_into(H_matrix &H, const char *path, int fmt) {
-    int32_t n = 0, m = 0, nnz = 0, reg = 0;
-    if (qldpc_load_matrix(path, fmt, &n, &m, &nnz, nullptr, nullptr, nullptr, nullptr, &reg))
-        throw std::runtime_error(qldpc_last_error());
-    std::vector<int32_t> rp(m + 1), ci(nnz), cp(n + 1), ri(nnz);
-    if (qldpc_load_matrix(path, fmt, &n, &m, &nnz, rp.data(), ci.data(), cp.data(), ri.data(), &reg))
-        throw std::runtime_error(qldpc_last_error());
-    H.check_nodes.assign(m, {});
-    for (int j = 0; j < m; ++j) H.check_nodes[j].assign(ci.begin() + rp[j], ci.begin() + rp[j + 1]);
-    H.bit_nodes.assign(n, {});
-    for (int i = 0; i < n; ++i) H.bit_nodes[i].assign(ri.begin() + cp[i], ri.begin() + cp[i + 1]);
-    H.is_regular = reg != 0;
-}
-
-std::vector<unsigned long long> read_u64(const char *path) {
-    std::ifstream in(path);
-    if (!in) throw std::runtime_error(std::string("cannot open ") + path);
-    std::vector<unsigned long long> v;
-    unsigned long long x;
-    while (in >> x) v.push_back(x);
-    return v;
-}
-
-std::vector<int> read_int(const char *path) {
-    std::vector<int> v;
-    for (unsigned long long x : read_u64(path)) v.push_back((int)x);
-    return v;
-}
+using namespace trial_common;
 
 struct trial_result {  // src/simulation.hpp: the fields run_trial fills
     LDPC_result ldpc_res{};
@@ -131,6 +94,31 @@ int main(int argc, char **argv) {
             size_t nnz = 0;
             for (const auto &r : H.check_nodes) nnz += r.size();
             std::printf("%zu %zu %zu\n", H.bit_nodes.size(), H.check_nodes.size(), nnz);
+            return 0;
+        }
+        if (mode == "badsyndrome" && argc >= 4) {
+            H_matrix H;
+            load_into(H, argv[2], std::atoi(argv[3]));
+            set_cfg("0", "50");
+            std::vector<double> llr(H.bit_nodes.size(), 3.0);
+            std::vector<int> synd(H.check_nodes.size(), 0), out(H.bit_nodes.size());
+            synd[1] = 2;
+            (void)sum_product_decoding(llr, H, synd, 50, 100.0, out);
+            std::printf("accepted\n");
+            return 0;
+        }
+        if (mode == "keycost" && argc >= 5) {
+            H_matrix H;
+            load_into(H, argv[2], std::atoi(argv[3]));
+            const int reps = std::atoi(argv[4]);
+            uint64_t sink = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int r = 0; r < reps; ++r) sink ^= qkd_ldpc_v_amd::impl::fast_key_of(H).sample;
+            const double fast = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            const auto t1 = std::chrono::steady_clock::now();
+            for (int r = 0; r < reps; ++r) sink ^= qkd_ldpc_v_amd::impl::key_of(H).h;
+            const double full = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count();
+            std::printf("keycost_us fast %.3f full %.3f %llu\n", fast / reps, full / reps, (unsigned long long)(sink & 1));
             return 0;
         }
         if (mode == "trials" && argc >= 10) {

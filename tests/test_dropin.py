@@ -146,3 +146,112 @@ def test_graph_cache_same_address_new_edges(gpu_available, tmp_path):
     lines = run(["reuse", matrix_path(name), 1, pB, 3, Q.SPA, 0, 0, 0.03, 50, sf], tmp_path)
     assert parse(lines, "A ") == oracle_trials(HA, Q.SPA, 0.0, 0.0, 0.03, 50, seeds)
     assert parse(lines, "B ") == oracle_trials(HB, Q.SPA, 0.0, 0.0, 0.03, 50, seeds)
+
+
+def test_dropin_refuses_non_bit_syndrome():
+    """The reference's decoders read syndrome[j] as a sign (any non-zero: -1,
+    src/qkd_ldpc_algorithm.cpp:57) and compare it by value (:101); the kernels
+    take bits, so the drop-in refuses a syndrome holding anything but 0 / 1,
+    before any device work (no GPU needed)."""
+    r = subprocess.run([_bin(), "badsyndrome", matrix_path("c1_n1024_m220.alist"), "1"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 1 and "syndrome[1] = 2 is not a bit" in r.stdout, r.stdout + r.stderr
+
+
+def test_graph_cache_fast_key_is_cheap():
+    """The cache's per-call key is O(1): a fingerprint of 128 sampled lists,
+    well under the full-content pass (which only a miss takes)."""
+    r = subprocess.run([_bin(), "keycost", matrix_path("c2_n10240_m2201.alist"), "1", "300"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    f = r.stdout.split()
+    fast, full = float(f[2]), float(f[4])
+    assert fast * 5 < full, (fast, full)
+
+
+# ---- the batch seam: QKD_LDPC_batch_simulation over the drop-in TUs ----------
+BATCH = os.path.join(ROOT, "tests", "dropin", "batch_check")
+
+
+def _batch_bin():
+    if not os.path.exists(BATCH):
+        pytest.fail(f"{BATCH} is not built (make)")
+    return BATCH
+
+
+def _stats_of(trials, n_trials):
+    """process_trials_results' decoding statistics (src/simulation.cpp:580-624)."""
+    it = np.array([t[0] for t in trials], np.float64)
+    ok = np.array([t[1] for t in trials], bool)
+    km = np.array([t[2] for t in trials], bool)
+    succ = it[ok]
+    mean = succ.mean() if succ.size else 0.0
+    std = np.sqrt(((succ - mean) ** 2).sum() / succ.size) if succ.size else 0.0
+    return (ok.sum() / n_trials, (ok & km).sum() / n_trials, int(succ.max()) if succ.size else 0,
+            int(succ.min()) if succ.size else 0, mean, std)
+
+
+def _run_batch(tmp_path, name, fmt, alg, prim, sec, qbers, max_it, trials, sim_seed, threads, H, punct=None,
+               short=None, devices="0,0,0"):
+    qf = tmp_path / "q.txt"
+    qf.write_text("\n".join(repr(float(q)) for q in qbers) + "\n")
+    files = [qf]
+    if punct is not None:
+        files += [write_list(tmp_path, "p.txt", punct), write_list(tmp_path, "s.txt", short)]
+    args = [_batch_bin(), "batch", matrix_path(name), fmt, alg, prim, sec, files[0], max_it, trials, sim_seed,
+            threads] + files[1:]
+    env = dict(os.environ, QKD_LDPC_HIP_DEVICES=devices, QLDPC_TRIAL_CHUNK="5")
+    r = subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.split("\n")
+    seeds = P.trial_seeds(sim_seed, trials)
+    for sim, q in enumerate(qbers):
+        sd = [(int(s) + sim) & 0xFFFFFFFFFFFFFFFF for s in seeds]
+        want = oracle_trials(H, alg, prim, sec, q, max_it, sd, punct, short)
+        seam = [tuple(int(x) for x in ln.split()[3:6]) for ln in lines if ln.startswith(f"S {sim} ")]
+        pert = [tuple(int(x) for x in ln.split()[3:6]) for ln in lines if ln.startswith(f"T {sim} ")]
+        assert seam == want, f"batch seam, combination {sim}"
+        assert pert == want, f"per-trial drop-in from {threads} threads, combination {sim}"
+        rt = [int(ln.split()[6]) for ln in lines if ln.startswith(f"S {sim} ")]
+        assert min(rt) >= 1
+        R = [ln.split() for ln in lines if ln.startswith(f"R {sim} ")]
+        assert len(R) == 1
+        dec, ldpc, it_max, it_min, it_mean, it_std = _stats_of(want, trials)
+        r_ = R[0]
+        assert float(r_[2]) == dec and float(r_[3]) == ldpc and int(r_[4]) == it_max and int(r_[5]) == it_min
+        assert float(r_[6]) == pytest.approx(it_mean, rel=1e-12) and float(r_[7]) == pytest.approx(it_std, rel=1e-9)
+        assert float(r_[8]) == int(H.n * q) / H.n
+        tp_mean, tp_std, tp_min, tp_max = (int(x) for x in r_[9:13])
+        assert 0 < tp_min <= tp_mean <= tp_max and tp_std >= 0
+    return lines
+
+
+@pytest.mark.gpu
+def test_batch_seam_qkd_ldpc_three_shards(gpu_available, tmp_path):
+    """QKD_LDPC_batch_simulation through the drop-in (adaptation off): every
+    trial of two combinations from the batch seam on a 3-logical-shard graph
+    (chunks of 5 trials, so both pipeline slots cycle), and from run_trial
+    called by 8 concurrent threads through the per-trial drop-in, equals the
+    oracle's run_trial; the aggregated sim_results equal the oracle's."""
+    name = "c1_n1024_m220.alist"
+    H = load_fixture(name)
+    _run_batch(tmp_path, name, 1, Q.NMSA, 0.78, 0.0, [0.02, 0.03], 50, 23, 9012025, 8, H)
+
+
+@pytest.mark.gpu
+def test_batch_seam_rate_adapt_three_shards(gpu_available, tmp_path):
+    """Adaptation on: the trials run QKD_LDPC_RATE_ADAPT (punctured draws from
+    the trial generator) on the R=0.8 format-3 code, AOMSA, 3 logical shards."""
+    name = "c5_n10240_m2048.sp2"
+    H = load_fixture(name)
+    u = np.array(gzip.open(matrix_path("c5_n10240_m2048.untp")).read().split(), np.int32)
+    punct, short, _ = Q.adapt_code_rate(H.n, H.m, 0.0156, 0.06, 1.39, u, Q.xoshiro_state(5555))
+    _run_batch(tmp_path, name, 3, Q.AOMSA, 0.7, 0.99, [0.0156], 50, 13, 5555, 8, H, punct, short)
+
+
+@pytest.mark.gpu
+def test_batch_seam_spa_c1_one_device(gpu_available, tmp_path):
+    """SPA with the default device list (every GPU of the box)."""
+    name = "c1_n1024_m220.alist"
+    H = load_fixture(name)
+    _run_batch(tmp_path, name, 1, Q.SPA, 0.0, 0.0, [0.025], 50, 16, 777, 4, H, devices="0")

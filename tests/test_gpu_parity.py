@@ -427,6 +427,14 @@ def test_device_qkd_ldpc_pipeline(gpu_available):
     assert np.array_equal(bits.cpu().numpy(), host.bits)
     assert np.array_equal(it.cpu().numpy().astype(np.uint32), host.iterations)
     assert np.array_equal(km.cpu().numpy(), (host.bits == a).all(axis=1).astype(np.uint8))
+    # no LLR workspace (the bench's form): the register decoder reads the
+    # builder's palette codes, the f64 LLRs are never written, same results
+    bits.zero_(), it.zero_(), km.zero_()
+    g.qkd_ldpc_device(p, ta, tb, lp, None, syn_ws, bits, it, ok, km)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits.cpu().numpy(), host.bits)
+    assert np.array_equal(it.cpu().numpy().astype(np.uint32), host.iterations)
+    assert np.array_equal(km.cpu().numpy(), (host.bits == a).all(axis=1).astype(np.uint8))
 
 
 def test_repeat_calls_deterministic(gpu_available):

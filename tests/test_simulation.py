@@ -3,6 +3,7 @@
 the GPU — whole simulations whose statistics are recomputed from the oracle."""
 import gzip
 import json
+import math
 import os
 import shutil
 
@@ -90,14 +91,13 @@ def test_adaptation_ranges_validation_mirrors_the_reference(tmp_path, field, val
 
 
 def test_driver_log_p_is_the_c_library_log():
-    """The driver's a-priori LLR magnitude is log((1-q)/q) by the C library, as
-    the reference computes it (src/qkd_ldpc_algorithm.cpp:1043): at n=10240,
-    n_err=229 numpy's log differs from it by one ulp on some hosts, which would
-    change every LLR of the frame."""
+    """The a-priori LLR magnitude qldpc_run_trials (the driver's seam) uses is
+    log((1-q)/q) by the C library, qldpc_log_p, as the reference computes it
+    (src/qkd_ldpc_algorithm.cpp:1043): at n=10240, n_err=229 numpy's log differs
+    from it by one ulp on some hosts, which would change every LLR of the frame."""
     for n, ne in ((10240, 229), (10240, 689), (102400, 2290), (102400, 5764), (1024, 13)):
         q = ne / n
         want = Q.log_p(q)
-        assert S.log_p(q) == want
         import ctypes
         libm = ctypes.CDLL("libm.so.6")
         libm.log.restype = ctypes.c_double
@@ -216,6 +216,8 @@ def test_simulation_end_to_end_matches_oracle(gpu_available, tmp_path):
     c = json.load(open(cfg_path("legacy_1k")))
     c["trials_number"] = 40
     c["code_rate_QBER_maps"] = [{"code_rate": 0.9, "QBER_begin": 0.02, "QBER_end": 0.03, "QBER_step": 0.01}]
+    c["enable_throughput_measurement"] = True
+    c["throughput_measurement_parameters"] = {"consider_RTT": False, "RTT": 0}
     cp = tmp_path / "c1.json"
     cp.write_text(json.dumps(c))
     cfg = S.Config.load(str(cp))
@@ -223,6 +225,8 @@ def test_simulation_end_to_end_matches_oracle(gpu_available, tmp_path):
     mats, combos = S.prepare(cfg, S.matrix_files(d))
     assert [x.config_qber for x in combos] == [0.02, 0.03]
     res = S.run(cfg, mats, combos, log=lambda *a: None)
+    for r in res:  # per-trial throughput distribution (src/simulation.cpp:626-681), not one amortised value
+        assert 0 < r["tp_min"] <= r["tp_mean"] <= r["tp_max"] and r["tp_std"] > 0 and r["tp_min"] < r["tp_max"]
     H = load_fixture("c1_n1024_m220.alist")
     seeds = Q.trial_seeds(cfg.simulation_seed, cfg.trials_number)
     for sim, (r, cb) in enumerate(zip(res, combos)):
@@ -254,3 +258,16 @@ def test_rate_adapted_simulation_matches_oracle(gpu_available, tmp_path):
         assert r["ratio_success_dec"] == ok.mean() and r["ratio_success_ldpc"] == (ok & km).mean()
         if ok.any():
             assert r["iter_mean"] == pytest.approx(it[ok].mean())
+
+
+def test_throughput_stats_restates_process_trials_results():
+    """THROUGHPUT_* (src/simulation.cpp:626-681): per-trial bits/s, mean and
+    population std over TRIALS_NUMBER, RTT added to each runtime, truncated."""
+    rt = np.array([10.0, 20.0, 40.0, 80.0])
+    mean, std, lo, hi = S.throughput_stats(8000, rt, 4)
+    tp = 8000 * 1e6 / rt
+    assert (mean, lo, hi) == (int(tp.mean()), int(tp.min()), int(tp.max()))
+    assert std == int(math.sqrt(((tp - tp.mean()) ** 2).mean()))
+    assert lo <= mean <= hi and std > 0
+    m2, _, lo2, hi2 = S.throughput_stats(8000, rt, 4, rtt_ms=0.4)
+    assert hi2 == int(8000 * 1e6 / (10.0 + 400.0)) and m2 < mean and lo2 < lo

@@ -69,12 +69,32 @@ def test_duplicate_bit_in_a_check_is_refused():
 
 
 def test_check_nodes_only_entries_refuse_unsorted_lists():
+    """The host-only planner takes check_nodes only; Graph(H, devices=...)
+    passes bit_nodes too (qldpc_graph_create_checked_on) — see the GPU test."""
     H = load_fixture("c1_n1024_m220.alist")
     Hu = permuted(H, 2, rows=False, cols=True)
     with pytest.raises(ValueError):
         Q.Graph(Hu, host_only=True)
-    with pytest.raises(ValueError):
-        Q.Graph(Hu, devices=[0])
+
+
+@pytest.mark.gpu
+def test_device_list_graph_keeps_occurrence_pairing(gpu_available):
+    """Graph(H, devices=[0, 0]) on unsorted bit_nodes: two logical shards, each
+    decoding with the reference's occurrence pairing, bit-exact vs the oracle."""
+    H = load_fixture("c1_n1024_m220.alist")
+    Hu = permuted(H, 2, rows=False, cols=True)
+    a, b, q = Q.bsc_frames(Hu.n, 0.03, 9, seed=77)
+    lp = Q.log_p(q)
+    llr = np.where(b != 0, -lp, lp).astype(np.float64)
+    synd = Hu.syndrome(a)
+    g = Q.Graph(Hu, devices=[0, 0])
+    assert g.info()["devices"] == 2
+    p = Q.Params(Q.SPA, 50, True, 100.0)
+    out = g.decode(p, llr, synd, posterior=True)
+    O = Oracle(Hu)
+    ob, oi, ok, op = O.decode_batch(O.params(Q.SPA, 50, True, 100.0), llr, synd, threads=8, posterior=True)
+    assert np.array_equal(out.bits, ob) and np.array_equal(out.iterations, oi) and np.array_equal(out.synd_ok, ok)
+    assert bits_equal_nan(out.posterior, op)
 
 
 def _parity(H, alg, prim, sec, batch, qber, max_it, seed):

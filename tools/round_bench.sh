@@ -16,5 +16,5 @@ run() {  # name, bench args
   if [ $rc -ne 0 ]; then echo "bench $name failed rc=$rc" >&2; tail -20 "$OUT/${TAG}_bench_$name.err" >&2; exit $rc; fi
 }
 if [ "${DEFAULT:-1}" = 1 ]; then run default; fi
-for wl in ${WLS:-c3 c5}; do run "$wl" --workload "$wl" --no-cpu-baseline; done
+for wl in ${WLS:-c3 c5}; do run "$wl" --workload "$wl" --cpu-baseline-seconds ${CPU_S:-8}; done
 echo "[$(date +%T)] done" >&2
