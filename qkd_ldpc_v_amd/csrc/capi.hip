@@ -99,7 +99,8 @@ struct TrialSlot {
     double *logp = nullptr;
     uint32_t *h_iters = nullptr;
     uint8_t *h_ok = nullptr, *h_km = nullptr;
-    uint64_t *h_clk = nullptr;
+    uint64_t *h_clk = nullptr, *h_seeds = nullptr;  // pinned: the copies stay asynchronous
+    double *h_logp = nullptr;
     size_t cap = 0, cap_punct = 0;
     int f0 = 0, nb = 0;  // the chunk in flight (nb == 0: none)
 };
@@ -1627,6 +1628,7 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(t.bits); (void)hipFree(t.ok); (void)hipFree(t.km); (void)hipFree(t.iters);
             (void)hipFree(t.tscratch); (void)hipFree(t.logp);
             (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
+            (void)hipHostFree(t.h_seeds); (void)hipHostFree(t.h_logp);
             if (t.ev0) (void)hipEventDestroy(t.ev0);
             if (t.ev1) (void)hipEventDestroy(t.ev1);
             if (t.stream) (void)hipStreamDestroy(t.stream);
@@ -2081,7 +2083,7 @@ int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const 
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, batch);
+    const size_t words = trials_scratch_words(n, n_err, batch);
     if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, n_punct, d_punct_alice,
                                  d_punct_bob, s);
@@ -2229,7 +2231,7 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, batch);
+    const size_t words = trials_scratch_words(n, n_err, batch);
     if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, 0, nullptr, nullptr, s);
     if (scratch) {
@@ -2263,11 +2265,15 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
     const double lp = qldpc_log_p(q_acc);  // log((1 - q) / q) by the host C library (:1043)
     const int n_punct = plan ? plan->n_punct : 0;
     // Frames per chunk: the slot's own buffers within ~512 MiB (QLDPC_TRIAL_CHUNK overrides).
-    const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 + (n > 65536 ? 4 * (size_t)n : 0);
-    int cap = (int)std::max<size_t>(1, std::min<size_t>(16384, ((size_t)512 << 20) / per_frame));
-    if (env_int("QLDPC_TRIAL_CHUNK", 0) > 0) cap = env_int("QLDPC_TRIAL_CHUNK", 0);
+    const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 + 4 * (size_t)trials_scratch_words(n, n_err, 1);
     const int G = (int)g->devs.size();
     const int per = (count + G - 1) / G;
+    // Frames per chunk: half a device's slice (>= 1024 frames), so generation of
+    // one chunk overlaps the decode of the other, within ~512 MiB of the slot's
+    // own buffers; QLDPC_TRIAL_CHUNK overrides.
+    int cap = (int)std::max<size_t>(1, std::min<size_t>(16384, ((size_t)512 << 20) / per_frame));
+    cap = std::min(cap, std::max(1024, (per + 1) / 2));
+    if (env_int("QLDPC_TRIAL_CHUNK", 0) > 0) cap = env_int("QLDPC_TRIAL_CHUNK", 0);
     std::vector<int> rcs(G, QLDPC_OK);
     std::vector<std::string> errs(G);
     auto work = [&](int gi) {
@@ -2277,7 +2283,6 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
         auto body = [&]() -> int {
             HIP_TRY(hipSetDevice(dg->device));
             std::lock_guard<std::mutex> lk(dg->trial_mu);
-            const std::vector<double> lpv((size_t)std::min(cap, hi - lo), lp);
             // results of a slot's chunk: wait for it, then each trial's share of
             // the chunk's window (QKD_LDPC's per-trial window on device, HIP
             // events on its stream) in proportion to its own decode span
@@ -2317,14 +2322,18 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                         (r = grow(&t.km, c)) || (r = grow(&t.iters, c)) || (r = grow(&t.logp, c)) ||
                         (r = grow(&t.palice, c * cp)) || (r = grow(&t.pbob, c * cp)))
                         return r;
-                    const size_t sw = trials_scratch_words(n, (int)c);
+                    const size_t sw = trials_scratch_words(n, n_err, (int)c);
                     if (sw && (r = grow(&t.tscratch, sw))) return r;
                     (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
+                    (void)hipHostFree(t.h_seeds); (void)hipHostFree(t.h_logp);
                     t.h_iters = nullptr; t.h_ok = nullptr; t.h_km = nullptr; t.h_clk = nullptr; t.cap = 0;
+                    t.h_seeds = nullptr; t.h_logp = nullptr;
                     HIP_TRY(hipHostMalloc(&t.h_iters, c * sizeof(uint32_t)));
                     HIP_TRY(hipHostMalloc(&t.h_ok, c));
                     HIP_TRY(hipHostMalloc(&t.h_km, c));
                     HIP_TRY(hipHostMalloc(&t.h_clk, 2 * c * sizeof(uint64_t)));
+                    HIP_TRY(hipHostMalloc(&t.h_seeds, c * sizeof(uint64_t)));
+                    HIP_TRY(hipHostMalloc(&t.h_logp, c * sizeof(double)));
                     t.cap = c;
                     t.cap_punct = cp;
                 }
@@ -2338,9 +2347,12 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                 const int nb = std::min(cap, hi - f);
                 if ((r = ensure(t, nb))) break;
                 auto enqueue = [&]() -> int {
-                    HIP_TRY(hipMemcpyAsync(t.seeds, seeds + f, (size_t)nb * sizeof(uint64_t), hipMemcpyHostToDevice,
+                    // (the slot's pinned inputs are free: its previous chunk was harvested)
+                    std::memcpy(t.h_seeds, seeds + f, (size_t)nb * sizeof(uint64_t));
+                    std::fill(t.h_logp, t.h_logp + nb, lp);
+                    HIP_TRY(hipMemcpyAsync(t.seeds, t.h_seeds, (size_t)nb * sizeof(uint64_t), hipMemcpyHostToDevice,
                                            t.stream));
-                    HIP_TRY(hipMemcpyAsync(t.logp, lpv.data(), (size_t)nb * sizeof(double), hipMemcpyHostToDevice,
+                    HIP_TRY(hipMemcpyAsync(t.logp, t.h_logp, (size_t)nb * sizeof(double), hipMemcpyHostToDevice,
                                            t.stream));
                     // run_trial's keys (+ QKD_LDPC_RATE_ADAPT's punctured draws), seed = seeds[n] + curr_sim (:743)
                     HIP_TRY(launch_trials(n, n_err, nb, t.seeds, seed_add, t.alice, t.bob, t.tscratch, n_punct,

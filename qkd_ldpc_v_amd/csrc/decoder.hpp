@@ -35,8 +35,13 @@ constexpr int V2_CODES_CAP = 20480;  // V2: bits per frame whose palette indices
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;
 // SPA-family register kernels at V2_R_TIGHT keep this many message slots in LDS
-// (when the frame's LDS image leaves room) instead of VGPRs.
-constexpr int V2_RL = 4;
+// (when the frame's LDS image leaves room) instead of VGPRs.  5: the C2 image
+// is then 159.8 KiB, and the kernel spills fewer VGPRs to scratch than with 4
+// (same-box A/B: 0.6% faster decode, profiles/r04/ab_rl5.txt).
+#ifndef QL_RL
+#define QL_RL 5
+#endif
+constexpr int V2_RL = QL_RL;
 // Workgroup size each V2 instantiation is compiled for (its VGPR budget).
 constexpr __host__ __device__ int v2_threads_for(int R) { return R <= V2_R_SMALL ? 1024 : 768; }
 
@@ -197,8 +202,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
                             uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
-size_t trials_lds_bytes(int n);
-size_t trials_scratch_words(int n, int batch);
+size_t trials_lds_bytes(int n, uint64_t n_err);
+size_t trials_scratch_words(int n, uint64_t n_err, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream);

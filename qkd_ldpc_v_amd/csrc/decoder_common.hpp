@@ -305,6 +305,37 @@ struct MetaSrcW : MetaSrc<R> {
             }
         }
     }
+    // Same, with the next group's two metadata words requested before this
+    // group's work.  For passes that store to global memory per slot (the VN
+    // stage of split frames and the hybrid shape): on gfx9 vmcnt counts stores
+    // too and drains in issue order, so a metadata load issued after a group's
+    // stores cannot be waited for without waiting for those stores; requested
+    // one group early, it waits only for the stores of the group before.
+    template <typename F>
+    __device__ __forceinline__ void each_upto2_pf(int epl_s, __amdgpu_buffer_rsrc_t rs2, F &&f) const {
+        asm volatile("" : "+s"(epl_s));
+        auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
+        auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rs2, this->voff, 0, 0);
+#pragma unroll
+        for (int g = 0; g < R / 4; ++g) {
+            rotate_prio(g);
+            if (4 * g < epl_s) {
+                const bool more = g + 1 < R / 4 && 4 * (g + 1) < epl_s;
+                const auto qn = more ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff,
+                                                                             (g + 1) * REG_TSTRIDE * 16, 0)
+                                     : q;
+                const auto q2n = more ? __builtin_amdgcn_raw_buffer_load_b128(rs2, this->voff,
+                                                                              (g + 1) * REG_TSTRIDE * 16, 0)
+                                      : q2;
+                f(4 * g + 0, (uint32_t)q[0], (uint32_t)q2[0]);
+                if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1], (uint32_t)q2[1]);
+                if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2], (uint32_t)q2[2]);
+                if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3], (uint32_t)q2[3]);
+                q = qn;
+                q2 = q2n;
+            }
+        }
+    }
     // Groups of four slots at least one of which is in the mask: f(g, q, bits)
     // with q the group's four metadata words and bits its 4-bit slice of the mask.
     template <typename F>

@@ -31,6 +31,9 @@ constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
 #define QL_VN_BATCH 2
 #endif
 constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS round trip
+#ifndef QL_MSG_PF
+#define QL_MSG_PF 1  // stage-writing message passes request the next group's metadata early
+#endif
 #ifdef QL_NO_ROWSCAN
 constexpr bool V2_ROWSCAN_ON = false;  // A/B only: SPA scan with per-slot flag bookkeeping
 #else
@@ -1201,7 +1204,9 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
                 emit(k, mt, mt2, c);
             };
-            if constexpr (GATHER || VNG) {
+            if constexpr (GATHER && QL_MSG_PF) {  // (global stage stores per slot)
+                meta.each_upto2_pf(epl, meta2_rs, message);
+            } else if constexpr (GATHER || VNG) {
                 meta.each_upto2(epl, meta2_rs, message);
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });

@@ -11,10 +11,16 @@
 // std::shuffle takes the two-swaps-per-draw path (__gen_two_uniform_ints)
 // because (2^64-1)/n >= n.
 //
-// Fisher-Yates is sequential, so one lane per trial runs it; the index vector
-// lives in LDS (uint16) for n <= 65536, in global scratch (uint32) above.
-// Many trials run concurrently (one 64-lane workgroup each); the other lanes
-// initialise the index vector and write the keys out coalesced.
+// Draws are sequential per trial, so each trial is one wave that runs its
+// generator chain wave-uniformly (scalar registers; one lane stores), many
+// trials at once.  inject_errors reads only the first k = floor(n*QBER)
+// positions of the shuffled index vector, and libstdc++'s std::shuffle is the
+// forward Fisher-Yates whose step at position i >= 1 swaps a[i] — still i,
+// untouched by the earlier steps — with some a[j], j <= i.  So positions >= k
+// never need storing: a step at i >= k only writes a[j] = i when j < k, and
+// only the steps at i < k swap inside the k-entry prefix.  The prefix lives in
+// LDS (global scratch when it does not fit); the same draws are consumed in
+// the same order, so the keys are the reference's bit for bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -65,79 +71,84 @@ __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
     return hi;
 }
 
-template <typename IDX, bool IN_LDS>
+template <bool PERM_LDS>
 __global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
                                                     uint64_t seed_add, uint8_t *alice, uint8_t *bob,
                                                     uint32_t *scratch, int n_punct, uint8_t *punct_alice,
                                                     uint8_t *punct_bob) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t tsm[];
     const int f = blockIdx.x;
     if (f >= batch) return;
     const int words = (n + 31) / 32;
-    uint32_t *abits = reinterpret_cast<uint32_t *>(smem);
+    const uint32_t k = (uint32_t)n_err;  // the shuffle's prefix that inject_errors reads
+    uint32_t *abits = tsm;
     uint32_t *flips = abits + words;
-    IDX *perm = IN_LDS ? reinterpret_cast<IDX *>(flips + words)
-                       : reinterpret_cast<IDX *>(scratch + (size_t)blockIdx.x * (size_t)n);
+    uint32_t *perm = PERM_LDS ? flips + words : scratch + (size_t)f * k;
     const int lane = threadIdx.x;
-    for (int i = lane; i < words; i += 64) {
-        abits[i] = 0;
-        flips[i] = 0;
-    }
-    if (n_err > 0)
-        for (int i = lane; i < n; i += 64) perm[i] = (IDX)i;
+    for (int i = lane; i < words; i += 64) flips[i] = 0;
+    for (uint32_t i = lane; i < k; i += 64) perm[i] = i;
     __syncthreads();
-    if (lane == 0) {
-        Xoshiro256pp g(seeds[f] + seed_add);
-        // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
-        // which never rejects: the top bit of each draw.
-        for (int w = 0; w < words; ++w) {
-            uint32_t v = 0;
-            const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
-            for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
-            abits[w] = v;
-        }
-        if (n_err > 0) {
-            // std::shuffle(first, last, g), libstdc++ 11 (bits/stl_algo.h)
-            uint64_t i = 1;
-            if ((n & 1) == 0) {
-                const uint64_t d = draw_below(g, 2);
-                const IDX t = perm[1];
-                perm[1] = perm[d];
-                perm[d] = t;
-                i = 2;
-            }
-            while (i != (uint64_t)n) {
-                const uint64_t b0 = i + 1, b1 = i + 2;  // __gen_two_uniform_ints(b0, b0 + 1)
-                const uint64_t x = draw_below(g, b0 * b1);
-                uint64_t p1, p2;
-                if (x < 0x100000000ull) {  // 32-bit divide when it fits (n <= 65535 always)
-                    const uint32_t x32 = (uint32_t)x, d32 = (uint32_t)b1;
-                    p1 = x32 / d32;
-                    p2 = x32 - (uint32_t)p1 * d32;
-                } else {
-                    p1 = x / b1;
-                    p2 = x % b1;
+    Xoshiro256pp g(seeds[f] + seed_add);
+    // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
+    // which never rejects: the top bit of each draw.
+    for (int w = 0; w < words; ++w) {
+        uint32_t v = 0;
+        const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
+        for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
+        if (lane == 0) abits[w] = v;
+    }
+    if (k > 0) {
+        // one swap of std::shuffle: a[pos] <-> a[p], p <= pos, on the k-prefix
+        auto swap_at = [&](uint32_t pos, uint32_t p) {
+            if (pos < k) {
+                const uint32_t t = perm[pos], u = perm[p];
+                if (lane == 0) {
+                    perm[pos] = u;
+                    perm[p] = t;
                 }
-                IDX t = perm[i];
-                perm[i] = perm[p1];
-                perm[p1] = t;
-                t = perm[i + 1];
-                perm[i + 1] = perm[p2];
-                perm[p2] = t;
-                i += 2;
+            } else if (p < k) {
+                if (lane == 0) perm[p] = pos;  // a[pos] == pos until its own step
             }
-            for (uint64_t e = 0; e < n_err; ++e) {
-                const uint32_t p = (uint32_t)perm[e];
-                flips[p >> 5] |= 1u << (p & 31);
-            }
+            __builtin_amdgcn_wave_barrier();  // (one wave: the next swap reads after these writes)
+        };
+        // std::shuffle(first, last, g), libstdc++ 11 (bits/stl_algo.h)
+        uint64_t i = 1;
+        if ((n & 1) == 0) {
+            swap_at(1, (uint32_t)draw_below(g, 2));
+            i = 2;
         }
-        // QKD_LDPC_RATE_ADAPT continues the trial's generator: two
-        // uniform_int_distribution<int>(0, 1) draws (Alice, then Bob) per
-        // punctured position, in ascending position order
-        // (src/qkd_ldpc_algorithm.cpp:1148-1157).
-        for (int j = 0; j < n_punct; ++j) {
-            punct_alice[(size_t)f * n_punct + j] = (uint8_t)(g.next() >> 63);
-            punct_bob[(size_t)f * n_punct + j] = (uint8_t)(g.next() >> 63);
+        while (i != (uint64_t)n) {
+            const uint64_t b0 = i + 1, b1 = i + 2;  // __gen_two_uniform_ints(b0, b0 + 1)
+            const uint64_t x = draw_below(g, b0 * b1);
+            uint64_t p1, p2;
+            if (x < 0x100000000ull) {  // 32-bit divide when it fits (n <= 65535 always)
+                const uint32_t x32 = (uint32_t)x, d32 = (uint32_t)b1;
+                p1 = x32 / d32;
+                p2 = x32 - (uint32_t)p1 * d32;
+            } else {
+                p1 = x / b1;
+                p2 = x % b1;
+            }
+            swap_at((uint32_t)i, (uint32_t)p1);
+            swap_at((uint32_t)i + 1, (uint32_t)p2);
+            i += 2;
+        }
+        __syncthreads();
+        for (uint32_t e = lane; e < k; e += 64) {
+            const uint32_t p = perm[e];
+            atomicOr(&flips[p >> 5], 1u << (p & 31));
+        }
+    }
+    // QKD_LDPC_RATE_ADAPT continues the trial's generator: two
+    // uniform_int_distribution<int>(0, 1) draws (Alice, then Bob) per
+    // punctured position, in ascending position order
+    // (src/qkd_ldpc_algorithm.cpp:1148-1157).
+    for (int j = 0; j < n_punct; ++j) {
+        const uint8_t pa = (uint8_t)(g.next() >> 63);
+        const uint8_t pb = (uint8_t)(g.next() >> 63);
+        if (lane == 0) {
+            punct_alice[(size_t)f * n_punct + j] = pa;
+            punct_bob[(size_t)f * n_punct + j] = pb;
         }
     }
     __syncthreads();
@@ -227,33 +238,33 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
     return hipGetLastError();
 }
 
-size_t trials_lds_bytes(int n) {
+// The k-entry shuffle prefix stays in LDS up to this size (else global scratch).
+constexpr size_t TRIALS_LDS_CAP = 64 * 1024;
+
+size_t trials_lds_bytes(int n, uint64_t n_err) {
     const size_t words = (size_t)(n + 31) / 32;
-    return 8 * words + (n <= 65536 ? 2 * (size_t)n : 0);
+    const size_t base = 8 * words, perm = 4 * (size_t)n_err;
+    return base + perm <= TRIALS_LDS_CAP ? base + perm : base;
 }
 
-size_t trials_scratch_words(int n, int batch) { return n <= 65536 ? 0 : (size_t)n * (size_t)batch; }
+size_t trials_scratch_words(int n, uint64_t n_err, int batch) {
+    const size_t words = (size_t)(n + 31) / 32;
+    return 8 * words + 4 * (size_t)n_err <= TRIALS_LDS_CAP ? 0 : (size_t)n_err * (size_t)batch;
+}
 
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    const size_t lds = trials_lds_bytes(n);
-    if (n <= 65536) {
-        auto k = trials_kernel<uint16_t, true>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
-                           scratch, n_punct, punct_alice, punct_bob);
-    } else {
-        auto k = trials_kernel<uint32_t, false>;
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob,
-                           scratch, n_punct, punct_alice, punct_bob);
-    }
+    const size_t lds = trials_lds_bytes(n, n_err);
+    const bool in_lds = trials_scratch_words(n, n_err, 1) == 0;
+    if (!in_lds && n_err > 0 && !scratch) return hipErrorInvalidValue;
+    auto k = in_lds ? trials_kernel<true> : trials_kernel<false>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob, scratch,
+                       n_punct, punct_alice, punct_bob);
     return hipGetLastError();
 }
 
