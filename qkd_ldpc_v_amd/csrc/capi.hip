@@ -101,7 +101,7 @@ struct TrialSlot {
     uint8_t *h_ok = nullptr, *h_km = nullptr;
     uint64_t *h_clk = nullptr, *h_seeds = nullptr;  // pinned: the copies stay asynchronous
     double *h_logp = nullptr;
-    size_t cap = 0, cap_punct = 0;
+    size_t cap = 0, cap_punct = 0, tscratch_words = 0;
     int f0 = 0, nb = 0;  // the chunk in flight (nb == 0: none)
 };
 
@@ -1712,16 +1712,14 @@ int qldpc_last_claim_order(qldpc_graph *g, int32_t device, void *stream, int32_t
     if (!g || !count) return fail(QLDPC_EINVAL, "graph / count is NULL");
     DeviceGraph *dg = find_dev(g, device);
     if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
-    int32_t *ord = nullptr, *wt = nullptr;
-    int cnt = 0;
-    {
-        std::lock_guard<std::mutex> lk(dg->mu);
-        auto it = dg->ws.find(stream);
-        if (it == dg->ws.end()) return fail(QLDPC_EINVAL, "no decode on that stream");
-        ord = it->second.forder;
-        wt = it->second.fweight;
-        cnt = it->second.order_count;
-    }
+    // (the workspace lock is held across the wait and the copies: a decode on
+    // the same stream with a larger batch would otherwise free and reallocate
+    // forder / fweight under the copy)
+    std::lock_guard<std::mutex> lk(dg->mu);
+    auto it = dg->ws.find(stream);
+    if (it == dg->ws.end()) return fail(QLDPC_EINVAL, "no decode on that stream");
+    int32_t *const ord = it->second.forder, *const wt = it->second.fweight;
+    const int cnt = it->second.order_count;
     *count = cnt;
     if (cnt == 0) return QLDPC_OK;
     if (cap < cnt) return fail(QLDPC_EINVAL, "order buffer smaller than the last batch");
@@ -2083,7 +2081,7 @@ int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const 
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, n_err, batch);
+    const size_t words = trials_scratch_words(n, n_err, n_punct, batch);
     if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, n_punct, d_punct_alice,
                                  d_punct_bob, s);
@@ -2231,7 +2229,7 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, n_err, batch);
+    const size_t words = trials_scratch_words(n, n_err, 0, batch);
     if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, 0, nullptr, nullptr, s);
     if (scratch) {
@@ -2265,7 +2263,8 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
     const double lp = qldpc_log_p(q_acc);  // log((1 - q) / q) by the host C library (:1043)
     const int n_punct = plan ? plan->n_punct : 0;
     // Frames per chunk: the slot's own buffers within ~512 MiB (QLDPC_TRIAL_CHUNK overrides).
-    const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 + 4 * (size_t)trials_scratch_words(n, n_err, 1);
+    const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 +
+                             4 * trials_scratch_words(n, n_err, n_punct, 64) / 64;
     const int G = (int)g->devs.size();
     const int per = (count + G - 1) / G;
     // Frames per chunk: half a device's slice (>= 1024 frames), so generation of
@@ -2322,8 +2321,7 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                         (r = grow(&t.km, c)) || (r = grow(&t.iters, c)) || (r = grow(&t.logp, c)) ||
                         (r = grow(&t.palice, c * cp)) || (r = grow(&t.pbob, c * cp)))
                         return r;
-                    const size_t sw = trials_scratch_words(n, n_err, (int)c);
-                    if (sw && (r = grow(&t.tscratch, sw))) return r;
+
                     (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
                     (void)hipHostFree(t.h_seeds); (void)hipHostFree(t.h_logp);
                     t.h_iters = nullptr; t.h_ok = nullptr; t.h_km = nullptr; t.h_clk = nullptr; t.cap = 0;
@@ -2336,6 +2334,13 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                     HIP_TRY(hipHostMalloc(&t.h_logp, c * sizeof(double)));
                     t.cap = c;
                     t.cap_punct = cp;
+                }
+                // the generator's workspace also grows with the error count k
+                const size_t sw = trials_scratch_words(n, n_err, n_punct, (int)t.cap);
+                if (sw > t.tscratch_words) {
+                    int r = grow(&t.tscratch, sw);
+                    if (r) return r;
+                    t.tscratch_words = sw;
                 }
                 return QLDPC_OK;
             };

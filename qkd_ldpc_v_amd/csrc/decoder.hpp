@@ -202,8 +202,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t *codes, double *palette,
                             uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
-size_t trials_lds_bytes(int n, uint64_t n_err);
-size_t trials_scratch_words(int n, uint64_t n_err, int batch);
+// Trial generator workspace (uint32 words) of `batch` trials.
+size_t trials_scratch_words(int n, uint64_t n_err, int n_punct, int batch);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream);

@@ -34,6 +34,9 @@ constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS roun
 #ifndef QL_MSG_PF
 #define QL_MSG_PF 1  // stage-writing message passes request the next group's metadata early
 #endif
+#ifndef QL_HOIST_LLR
+#define QL_HOIST_LLR 0  // (A/B) SPA message pass: the kpos-0 channel LLR requested first
+#endif
 #ifdef QL_NO_ROWSCAN
 constexpr bool V2_ROWSCAN_ON = false;  // A/B only: SPA scan with per-slot flag bookkeeping
 #else
@@ -1162,6 +1165,16 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     if (k > 0) r += (mt & META_START) ? 1 : 0;
                 }
                 double c;
+                // SPA on one-workgroup register shapes: a kpos-0 edge's channel
+                // LLR (two dependent LDS reads) is requested before the message
+                // math, so its latency hides behind it (VN phase 0 below)
+                constexpr bool HOIST = QL_HOIST_LLR && ALG == 0 && !SPLIT && !VNG && !GATHER;
+                bool kpos0 = false;
+                double lv0 = 0.0;
+                if constexpr (HOIST) {
+                    kpos0 = __builtin_amdgcn_inverse_ballot_w64(vn_exec[k]);
+                    if (kpos0) lv0 = llr_of((int)(mt & META_COL_MASK));
+                }
                 if constexpr (ALG == 0) {
                     // 2. * atanh(rp / t) (:66-68) and the clip (:73-74) in one
                     const double ra = rowA[r], tk = c2b.get_seq(k);
@@ -1202,7 +1215,12 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     }
                 }
                 if constexpr (SPA_FAM && ALG != 0) c = clip_msg(c, thr);  // (:73-74)
-                emit(k, mt, mt2, c);
+                if constexpr (HOIST) {
+                    c2b.set(k, c);
+                    if (kpos0) tot_at(mt) = lv0 + c;  // first term of std::accumulate (:78)
+                } else {
+                    emit(k, mt, mt2, c);
+                }
             };
             if constexpr (GATHER && QL_MSG_PF) {  // (global stage stores per slot)
                 meta.each_upto2_pf(epl, meta2_rs, message);

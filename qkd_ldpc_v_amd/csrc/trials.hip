@@ -11,16 +11,20 @@
 // std::shuffle takes the two-swaps-per-draw path (__gen_two_uniform_ints)
 // because (2^64-1)/n >= n.
 //
-// Draws are sequential per trial, so each trial is one wave that runs its
-// generator chain wave-uniformly (scalar registers; one lane stores), many
-// trials at once.  inject_errors reads only the first k = floor(n*QBER)
-// positions of the shuffled index vector, and libstdc++'s std::shuffle is the
-// forward Fisher-Yates whose step at position i >= 1 swaps a[i] — still i,
-// untouched by the earlier steps — with some a[j], j <= i.  So positions >= k
-// never need storing: a step at i >= k only writes a[j] = i when j < k, and
-// only the steps at i < k swap inside the k-entry prefix.  The prefix lives in
-// LDS (global scratch when it does not fit); the same draws are consumed in
-// the same order, so the keys are the reference's bit for bit.
+// Draws are sequential per trial, so each LANE runs one trial's generator
+// chain (64 trials per wave, their state in VGPRs, every lane taking the same
+// control flow: the shuffle's loop positions are the same for all trials).
+// inject_errors reads only the first k = floor(n*QBER) positions of the
+// shuffled index vector, and libstdc++'s std::shuffle is the forward
+// Fisher-Yates whose step at position i >= 1 swaps a[i] — still i, untouched
+// by the earlier steps — with some a[j], j <= i.  So positions >= k never need
+// storing: a step at i >= k only writes a[j] = i when j < k, and only the
+// steps at i < k swap inside the k-entry prefix.  Per-trial words (Alice's
+// bits, the flips, the prefix, the punctured draws) live in a global
+// workspace interleaved [word][lane] (a wave's access to one word index is one
+// 256-byte line); a second kernel expands them into the byte keys, one
+// workgroup per trial.  The same draws are consumed in the same order, so the
+// keys are the reference's bit for bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -71,45 +75,50 @@ __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
     return hi;
 }
 
-template <bool PERM_LDS>
-__global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
-                                                    uint64_t seed_add, uint8_t *alice, uint8_t *bob,
-                                                    uint32_t *scratch, int n_punct, uint8_t *punct_alice,
-                                                    uint8_t *punct_bob) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t tsm[];
-    const int f = blockIdx.x;
-    if (f >= batch) return;
-    const int words = (n + 31) / 32;
-    const uint32_t k = (uint32_t)n_err;  // the shuffle's prefix that inject_errors reads
-    uint32_t *abits = tsm;
-    uint32_t *flips = abits + words;
-    uint32_t *perm = PERM_LDS ? flips + words : scratch + (size_t)f * k;
+// Words of one trial's workspace column: Alice's bits, the flips, the
+// k-prefix and the punctured draws (Alice's, Bob's) as bit words.
+struct TrialWs {
+    int words, k, pwords;
+    __host__ __device__ TrialWs(int n, uint64_t n_err, int n_punct)
+        : words((n + 31) / 32), k((int)n_err), pwords((n_punct + 31) / 32) {}
+    __host__ __device__ size_t per_lane() const { return 2 * (size_t)words + (size_t)k + 2 * (size_t)pwords; }
+    __host__ __device__ size_t abits() const { return 0; }
+    __host__ __device__ size_t flips() const { return (size_t)words; }
+    __host__ __device__ size_t perm() const { return 2 * (size_t)words; }
+    __host__ __device__ size_t palice() const { return 2 * (size_t)words + (size_t)k; }
+    __host__ __device__ size_t pbob() const { return 2 * (size_t)words + (size_t)k + (size_t)pwords; }
+};
+
+__global__ void __launch_bounds__(64) trials_lanes_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
+                                                          uint64_t seed_add, uint32_t *ws, int n_punct) {
     const int lane = threadIdx.x;
-    for (int i = lane; i < words; i += 64) flips[i] = 0;
-    for (uint32_t i = lane; i < k; i += 64) perm[i] = i;
-    __syncthreads();
-    Xoshiro256pp g(seeds[f] + seed_add);
+    const int f = blockIdx.x * 64 + lane;
+    const TrialWs L(n, n_err, n_punct);
+    // this wave's 64 columns, [word][lane]
+    uint32_t *col = ws + (size_t)blockIdx.x * L.per_lane() * 64 + lane;
+    auto at = [&](size_t word) -> uint32_t & { return col[word * 64]; };
+    Xoshiro256pp g((f < batch ? seeds[f] : 0ull) + seed_add);
     // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
     // which never rejects: the top bit of each draw.
-    for (int w = 0; w < words; ++w) {
+    for (int w = 0; w < L.words; ++w) {
         uint32_t v = 0;
         const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
         for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
-        if (lane == 0) abits[w] = v;
+        at(L.abits() + w) = v;
+        at(L.flips() + w) = 0u;
     }
+    const uint32_t k = (uint32_t)n_err;
     if (k > 0) {
-        // one swap of std::shuffle: a[pos] <-> a[p], p <= pos, on the k-prefix
+        for (uint32_t e = 0; e < k; ++e) at(L.perm() + e) = e;
+        // one swap of std::shuffle, a[pos] <-> a[p] (p <= pos), on the k-prefix
         auto swap_at = [&](uint32_t pos, uint32_t p) {
-            if (pos < k) {
-                const uint32_t t = perm[pos], u = perm[p];
-                if (lane == 0) {
-                    perm[pos] = u;
-                    perm[p] = t;
-                }
+            if (pos < k) {  // (pos is the same on every lane)
+                const uint32_t t = at(L.perm() + pos), u = at(L.perm() + p);
+                at(L.perm() + pos) = u;
+                at(L.perm() + p) = t;
             } else if (p < k) {
-                if (lane == 0) perm[p] = pos;  // a[pos] == pos until its own step
+                at(L.perm() + p) = pos;  // a[pos] == pos until its own step
             }
-            __builtin_amdgcn_wave_barrier();  // (one wave: the next swap reads after these writes)
         };
         // std::shuffle(first, last, g), libstdc++ 11 (bits/stl_algo.h)
         uint64_t i = 1;
@@ -133,32 +142,47 @@ __global__ void __launch_bounds__(64) trials_kernel(int n, uint64_t n_err, int b
             swap_at((uint32_t)i + 1, (uint32_t)p2);
             i += 2;
         }
-        __syncthreads();
-        for (uint32_t e = lane; e < k; e += 64) {
-            const uint32_t p = perm[e];
-            atomicOr(&flips[p >> 5], 1u << (p & 31));
+        for (uint32_t e = 0; e < k; ++e) {  // inject_errors: flip pos[0 .. k)
+            const uint32_t p = at(L.perm() + e);
+            at(L.flips() + (p >> 5)) |= 1u << (p & 31);
         }
     }
     // QKD_LDPC_RATE_ADAPT continues the trial's generator: two
     // uniform_int_distribution<int>(0, 1) draws (Alice, then Bob) per
     // punctured position, in ascending position order
     // (src/qkd_ldpc_algorithm.cpp:1148-1157).
-    for (int j = 0; j < n_punct; ++j) {
-        const uint8_t pa = (uint8_t)(g.next() >> 63);
-        const uint8_t pb = (uint8_t)(g.next() >> 63);
-        if (lane == 0) {
-            punct_alice[(size_t)f * n_punct + j] = pa;
-            punct_bob[(size_t)f * n_punct + j] = pb;
+    for (int w = 0; w < L.pwords; ++w) {
+        uint32_t va = 0, vb = 0;
+        const int nb = (n_punct - 32 * w < 32) ? n_punct - 32 * w : 32;
+        for (int b = 0; b < nb; ++b) {
+            va |= (uint32_t)(g.next() >> 63) << b;
+            vb |= (uint32_t)(g.next() >> 63) << b;
         }
+        at(L.palice() + w) = va;
+        at(L.pbob() + w) = vb;
     }
-    __syncthreads();
+}
+
+// The keys as bytes, one workgroup per trial: Alice's, Bob's (Alice's xor the
+// flips) and the punctured draws.
+__global__ void __launch_bounds__(256) trials_expand_kernel(int n, uint64_t n_err, int batch, const uint32_t *ws,
+                                                            uint8_t *alice, uint8_t *bob, int n_punct,
+                                                            uint8_t *punct_alice, uint8_t *punct_bob) {
+    const int f = blockIdx.x;
+    const TrialWs L(n, n_err, n_punct);
+    const uint32_t *col = ws + (size_t)(f / 64) * L.per_lane() * 64 + (f % 64);
+    auto at = [&](size_t word) { return col[word * 64]; };
     uint8_t *a = alice + (size_t)f * n;
     uint8_t *b = bob + (size_t)f * n;
-    for (int i = lane; i < n; i += 64) {
-        const uint32_t av = (abits[i >> 5] >> (i & 31)) & 1u;
-        const uint32_t fv = (flips[i >> 5] >> (i & 31)) & 1u;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t av = (at(L.abits() + (i >> 5)) >> (i & 31)) & 1u;
+        const uint32_t fv = (at(L.flips() + (i >> 5)) >> (i & 31)) & 1u;
         a[i] = (uint8_t)av;
         b[i] = (uint8_t)(av ^ fv);
+    }
+    for (int j = threadIdx.x; j < n_punct; j += blockDim.x) {
+        punct_alice[(size_t)f * n_punct + j] = (uint8_t)((at(L.palice() + (j >> 5)) >> (j & 31)) & 1u);
+        punct_bob[(size_t)f * n_punct + j] = (uint8_t)((at(L.pbob() + (j >> 5)) >> (j & 31)) & 1u);
     }
 }
 
@@ -238,32 +262,20 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
     return hipGetLastError();
 }
 
-// The k-entry shuffle prefix stays in LDS up to this size (else global scratch).
-constexpr size_t TRIALS_LDS_CAP = 64 * 1024;
-
-size_t trials_lds_bytes(int n, uint64_t n_err) {
-    const size_t words = (size_t)(n + 31) / 32;
-    const size_t base = 8 * words, perm = 4 * (size_t)n_err;
-    return base + perm <= TRIALS_LDS_CAP ? base + perm : base;
-}
-
-size_t trials_scratch_words(int n, uint64_t n_err, int batch) {
-    const size_t words = (size_t)(n + 31) / 32;
-    return 8 * words + 4 * (size_t)n_err <= TRIALS_LDS_CAP ? 0 : (size_t)n_err * (size_t)batch;
+size_t trials_scratch_words(int n, uint64_t n_err, int n_punct, int batch) {
+    return TrialWs(n, n_err, n_punct).per_lane() * 64 * (size_t)((batch + 63) / 64);
 }
 
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    const size_t lds = trials_lds_bytes(n, n_err);
-    const bool in_lds = trials_scratch_words(n, n_err, 1) == 0;
-    if (!in_lds && n_err > 0 && !scratch) return hipErrorInvalidValue;
-    auto k = in_lds ? trials_kernel<true> : trials_kernel<false>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    if (!scratch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(trials_lanes_kernel, dim3((batch + 63) / 64), dim3(64), 0, stream, n, n_err, batch, seeds,
+                       seed_add, scratch, n_punct);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(batch), dim3(64), lds, stream, n, n_err, batch, seeds, seed_add, alice, bob, scratch,
+    hipLaunchKernelGGL(trials_expand_kernel, dim3(batch), dim3(256), 0, stream, n, n_err, batch, scratch, alice, bob,
                        n_punct, punct_alice, punct_bob);
     return hipGetLastError();
 }

@@ -17,5 +17,8 @@ for f in "c1_n1024_m220.alist 1" "c2_n10240_m2201.alist 1" "c5_n10240_m2048.sp2 
   build/asan/host_mirror_check load $M/$name.gz $fmt
   build/asan/run_trial_check load $M/$name.gz $fmt
 done
+echo "== drop-in graph-cache keys and the syndrome check (host-only)"
+build/asan/run_trial_check keycost $M/c2_n10240_m2201.alist.gz 1 50
+if build/asan/run_trial_check badsyndrome $M/c1_n1024_m220.alist.gz 1; then echo "bad syndrome accepted" >&2; exit 1; fi
 echo "== pytest -m 'not gpu' on the ASan libraries"
 LD_PRELOAD=$RT QLDPC_ASAN=1 python -m pytest tests -q -m "not gpu" -p no:cacheprovider -x "$@"
