@@ -77,6 +77,48 @@ def py_trial(n, qber, seed):
     return np.array(a, np.uint8), np.array(b, np.uint8), ne / n
 
 
+def py_trial_prefix(n, qber, seed):
+    """The device generator's form (trials.hip): the same draws, but the
+    shuffle keeps only the k = floor(n*qber) prefix inject_errors reads — a
+    swap at position pos >= k only writes a[p] = pos when p < k (a[pos] is
+    still pos then)."""
+    g = PyXoshiro(seed)
+    a = [py_below(g, 2) for _ in range(n)]
+    k = int(float(n) * qber)
+    pre = list(range(k))
+
+    def swap(pos, p):
+        if pos < k:
+            pre[pos], pre[p] = pre[p], pre[pos]
+        elif p < k:
+            pre[p] = pos
+
+    if k > 0:
+        i = 1
+        if n % 2 == 0:
+            swap(1, py_below(g, 2))
+            i = 2
+        while i != n:
+            b0 = i + 1
+            x = py_below(g, b0 * (b0 + 1))
+            swap(i, x // (b0 + 1))
+            swap(i + 1, x % (b0 + 1))
+            i += 2
+    b = list(a)
+    for p in pre:
+        b[p] ^= 1
+    return np.array(a, np.uint8), np.array(b, np.uint8)
+
+
+@pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (2048, 0.0005, 77),
+                                         (1025, 0.3, 9), (10240, 0.013, 1022025)])
+def test_prefix_shuffle_equals_full_shuffle(n, qber, seed):
+    """The k-prefix shuffle the device runs gives the full shuffle's keys."""
+    a, b, _ = py_trial(n, qber, seed)
+    pa, pb = py_trial_prefix(n, qber, seed)
+    assert np.array_equal(a, pa) and np.array_equal(b, pb)
+
+
 @pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (10240, 0.013, 1022025)])
 def test_oracle_trial_matches_python_restatement(n, qber, seed):
     a, b, q = P.trial(n, qber, seed)
@@ -94,11 +136,12 @@ def test_seed_sequences_agree():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,qber", [(1024, 0.013), (10240, 0.0215), (10241, 0.05), (102400, 0.038)])
-def test_device_trials_bitexact(gpu_available, n, qber):
+@pytest.mark.parametrize("n,qber,batch", [(1024, 0.013, 24), (1024, 0.0015, 130), (10240, 0.0215, 24),
+                                           (10241, 0.05, 24), (102400, 0.038, 4)])
+def test_device_trials_bitexact(gpu_available, n, qber, batch):
+    """(batch 130: three waves of the one-trial-per-lane generator, the last partial)"""
     import torch
 
-    batch = 24 if n < 100000 else 4
     seeds = Q.trial_seeds(9012025, batch)
     d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()
     da = torch.empty((batch, n), dtype=torch.uint8, device="cuda")

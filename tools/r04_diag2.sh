@@ -10,4 +10,5 @@ timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_ACTIVE_INST_VALU SQ_INSTS
   -d $O/vb -o run --output-format csv -- tools/valu_bench > $O/vb.log 2>&1 || { tail -5 $O/vb.log; exit 11; }
 POINTS="2 20" timeout -k 10 400 tools/stamps_c5.sh || exit 12
 VARS="cur hoist" WLS=c2 REPS=2 STEPS=6 timeout -k 10 400 tools/ab_builds.sh || exit 13
+QLDPC_SPLIT_K=16 WLS=c4 timeout -k 10 300 tools/stamps.sh || exit 14
 echo done
