@@ -119,6 +119,8 @@ struct DeviceGraph {
     int32_t *hd_bits = nullptr, *hd_dv = nullptr, *stage_off = nullptr;
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
     int32_t *part_row0 = nullptr; // V2 split: first layout row of each part
+    int32_t *xoff = nullptr;      // V2 split exchange: region starts
+    uint16_t *xbit = nullptr, *xbit_ms = nullptr;  // ... chunk-local bit per stage position (CSR / kpos layouts)
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
     uint32_t *vng_bits = nullptr, *vng_meta2 = nullptr;  // hybrid bit gather: bit order, slot positions
@@ -200,6 +202,7 @@ struct qldpc_graph {
     int nst_max = 0;                        // V2 SPA scan: most rows started in one lane (row_rmask rows)
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
+    int split_cb = 0, split_nc = 0;         // V2 split exchange gather: bits per LDS chunk, chunks per part (0: off)
     bool kernel_timing = false;             // qldpc_set_kernel_timing
     std::vector<int32_t> col_lab;           // V2 bank relabelling (relabel.cpp): bit id -> label; empty: identity
     long long relabel_stats[4] = {0, 0, 0, 0};  // bank excess before / after, busiest-bank cycles before / after
@@ -224,7 +227,8 @@ int block_threads(const qldpc_graph &g) {
 }
 
 size_t lds_of(const qldpc_graph &g, int alg) {
-    if (g.variant == VAR_V2 && g.split_k > 1) return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true);
+    if (g.variant == VAR_V2 && g.split_k > 1)
+        return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true, 0, 0, -1, g.split_cb);
     return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG,
                                               (g.rows_global_ms && alg >= 2) ? g.rows_lds_ms : -1)
                                : lds_bytes_for(g.variant, g.n, g.m, g.T);
@@ -529,6 +533,30 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr) {
         g.split_k = K;
         g.split_mrows = mrows;
         g.part_row0 = prow;
+        // Exchange gather (DecodeArgs::xoff): the largest LDS chunk of a part's
+        // bits every algorithm's layout holds (SPA keeps its LDS message slots
+        // when they fit without it), split evenly; QLDPC_SPLIT_X=0: the
+        // term-major stage (A/B).
+        g.split_cb = g.split_nc = 0;
+        if (env_int("QLDPC_SPLIT_X", 1)) {
+            const int own = (g.n + K - 1) / K;
+            const bool rl0 = v2_split_rl_fits(g.n, mrows, 0);
+            auto fits = [&](int cb) {
+                return lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, cb) <= LDS_LIMIT &&
+                       lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, cb) <= LDS_LIMIT &&
+                       (!rl0 || v2_split_rl_fits(g.n, mrows, cb));
+            };
+            int lo = 0, hi = std::min(own, 0xFFFF);
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2;
+                if (fits(mid)) lo = mid;
+                else hi = mid - 1;
+            }
+            if (lo >= 256) {
+                g.split_nc = (own + lo - 1) / lo;
+                g.split_cb = (own + g.split_nc - 1) / g.split_nc;
+            }
+        }
         return true;
     }
     return false;
@@ -1015,6 +1043,49 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     int brc = build_meta(false, meta, vnm, meta2, vex);
     if (!brc && v2) brc = build_meta(true, meta_ms, vnm_ms, meta2_ms, vex_ms);
     if (brc) return brc;
+    // Split frames' exchange layout (DecodeArgs::xoff): each staged term's
+    // region is (owner part of its bit, chunk, kpos); inside a region the terms
+    // follow (writer wave, slot, lane), so the stage position of every slot is
+    // assigned walking the slots in that order.  Region sizes depend only on
+    // the edges, so both slot layouts (CSR, kpos-sorted) share xoff.
+    std::vector<int32_t> xoff;
+    std::vector<uint16_t> xbit, xbit_ms;
+    if (v2 && g->split_k > 1 && g->split_cb > 0) {
+        const int K = g->split_k, NC = g->split_nc, CB = g->split_cb, D = g->dv_max;
+        std::vector<int32_t> reg0(n), lbit(n);
+        for (int p = 0; p < K; ++p) {
+            const int lo = (int)((long long)n * p / K), hi = (int)((long long)n * (p + 1) / K);
+            for (int b = lo; b < hi; ++b) {
+                const int c = (b - lo) / CB;
+                reg0[b] = (p * NC + c) * D;
+                lbit[b] = (b - lo) - c * CB;
+            }
+        }
+        const size_t NR = (size_t)K * NC * D;
+        std::vector<long long> fill(NR + 1, 0);
+        for (int e = 0; e < E; ++e) ++fill[(size_t)reg0[col_idx[e]] + kpos[e] + 1];
+        for (size_t r = 0; r < NR; ++r) fill[r + 1] += fill[r];
+        if (fill[NR] != g->stage_doubles) return fail(QLDPC_EUNSUP, "split exchange layout: term count");
+        xoff.assign(fill.begin(), fill.end());
+        fill.pop_back();
+        auto assign = [&](const std::vector<uint32_t> &mt, std::vector<uint32_t> &mt2, std::vector<uint16_t> &xb) {
+            std::vector<long long> pos(fill);
+            xb.assign((size_t)g->stage_doubles, 0);
+            for (int w = 0; w < W; ++w)
+                for (int k = 0; k < S4; ++k)
+                    for (int li = 0; li < 64; ++li) {
+                        const size_t i = midx(w * 64 + li, k);
+                        const uint32_t kp = (mt[i] >> META_KPOS_SHIFT) & META_KPOS_MASK;
+                        if (kp == META_KPOS_MASK) continue;  // dummy slot
+                        const int b = (int)(mt[i] & META_COL_MASK);
+                        const long long q = pos[(size_t)reg0[b] + kp]++;
+                        mt2[i] = (uint32_t)q;
+                        xb[(size_t)q] = (uint16_t)lbit[b];
+                    }
+        };
+        assign(meta, meta2, xbit);
+        assign(meta_ms, meta2_ms, xbit_ms);
+    }
     g->nst_max = row_sem.empty() ? 0 : nst_max;
     if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
         auto visited = [&](const std::vector<uint64_t> &v) {
@@ -1028,9 +1099,9 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         fprintf(stderr, "{\"plan\": {\"waves\": %d, \"slots_reg\": %d, \"slots_scratch\": %d, \"epl_max\": %d, "
                         "\"dv_max\": %d, \"vn_slot_visits_csr\": %lld, \"vn_slot_visits_kpos_sorted\": %lld, "
                         "\"vn_slot_visits_unmasked\": %lld, \"rows_global_ms\": %d, \"rows_lds_ms\": %d, "
-                        "\"rows_lds_waves_ms\": %d}}\n",
+                        "\"rows_lds_waves_ms\": %d, \"split_k\": %d, \"split_cb\": %d, \"split_nc\": %d}}\n",
                 W, g->v2R, g->v2RG, g->EPL, g->dv_max, visited(vnm), visited(vnm_ms), full, (int)g->rows_global_ms,
-                g->rows_lds_ms, g->rows_lds_waves_ms);
+                g->rows_lds_ms, g->rows_lds_waves_ms, g->split_k, g->split_cb, g->split_nc);
         fprintf(stderr, "{\"relabel\": {\"excess_before\": %lld, \"excess_after\": %lld, \"cycles_before\": %lld, "
                         "\"cycles_after\": %lld}}\n",
                 g->relabel_stats[0], g->relabel_stats[1], g->relabel_stats[2], g->relabel_stats[3]);
@@ -1088,7 +1159,8 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->slot_meta2, meta2)) || (rc = upload(&dg->slot_meta2_ms, meta2_ms)) ||
             (rc = upload(&dg->hd_bits, hd_bits)) || (rc = upload(&dg->hd_dv, hd_dv)) ||
             (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
-            (rc = upload(&dg->part_row0, g->part_row0)) ||
+            (rc = upload(&dg->part_row0, g->part_row0)) || (rc = upload(&dg->xoff, xoff)) ||
+            (rc = upload(&dg->xbit, xbit)) || (rc = upload(&dg->xbit_ms, xbit_ms)) ||
             (rc = upload(&dg->lane_row0, lrow0)) || (rc = upload(&dg->wave_rows, g->wave_rows)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
@@ -1326,6 +1398,10 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         a.gtotal = w->gtotal;
         a.gstage = w->gstage;
         a.stage_frame_doubles = g->stage_doubles;
+        a.split_cb = g->split_cb;
+        a.split_nc = g->split_nc;
+        a.xoff = g->split_cb > 0 ? dg->xoff : nullptr;
+        a.xbit = alg >= 2 ? dg->xbit_ms : dg->xbit;
         HIP_TRY(hipMemsetAsync(w->split_ctl, 0, (32 + 3 * 16 * (size_t)slots) * sizeof(int), stream));
     }
     a.nc = (g->n + 3) / 4;
@@ -1590,6 +1666,9 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->stage_off);
         (void)hipFree(d->row_orig);
         (void)hipFree(d->part_row0);
+        (void)hipFree(d->xoff);
+        (void)hipFree(d->xbit);
+        (void)hipFree(d->xbit_ms);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->vn_exec);

@@ -124,6 +124,15 @@ struct DecodeArgs {
     int *split_err;                 // set when a part group failed to meet (results void)
     double *gstage;                 // [batch][stage_frame_doubles] split frames' VN stage
     long long stage_frame_doubles;
+    // Split-frame exchange layout (nullptr xoff: the term-major stage).  Part p
+    // owns bits [n p / K, n (p + 1) / K) in split_nc chunks of split_cb; the
+    // stage is one region per (owner part, chunk, kpos), each holding its terms
+    // in (writer wave, slot, lane) order, so a writing wave fills whole lines
+    // and the owner reads each region front to back, adding every term into
+    // an LDS sum at the bit's chunk-local index xbit[position].
+    int split_cb, split_nc;
+    const int32_t *xoff;            // [K * nc * dv_max + 1] region starts (doubles into the frame's stage)
+    const uint16_t *xbit;           // [stage_frame_doubles] chunk-local bit of each stage position
     // v1 global-slot kernels, unsorted adjacency (occurrence pairing): input
     // slot s of the next check-node pass gets total[pair_col[s]] -
     // c2b[pair_src[s]] (both [k][lane]); the values go through a slot-major
@@ -192,11 +201,14 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
 
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
 // rows_lds: min-sum row aggregates kept in LDS on the hybrid shape (-1: all m).
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0, int rows_lds = -1);
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0, int rows_lds = -1,
+                    int gcb = 0);
 // Whether a V2 shape can run the min-sum bit gather (DecodeArgs::vn_rows):
 // the dv <= 4 register shape, or the hybrid shape when the padded edge
 // positions' two code bits fit the LDS byte area.
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m);
+// Split frames: whether the SPA layout keeps its LDS message slots at gcb exchange-gather bits.
+bool v2_split_rl_fits(int n, int mrows, int gcb);
 constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per lane for dummy slots
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);

@@ -64,7 +64,7 @@ constexpr int V2_A0_ENTRIES = 64;
 struct V2Layout {
     size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, syn, bytes;
     __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0,
-                                 bool rowscan = false) {
+                                 bool rowscan = false, int gcb = 0) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
@@ -74,6 +74,9 @@ struct V2Layout {
         tail = o;     // (min-sum: a lane's tail aggregate is parked in its row's rowAB entry)
         tailneg = o;
         a0tab = o; o = al16(o + (minsum ? 0 : (size_t)V2_A0_ENTRIES * 8));  // SPA: iteration-0 table
+        // split frames' exchange gather: gcb bit sums in LDS over the rows and
+        // the iteration-0 table, both dead between the message pass and the scan
+        if (split && gcb > 0 && al16(rows + (size_t)gcb * 8) > o) o = al16(rows + (size_t)gcb * 8);
         ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * (sizeof(ql_exact::Expm1A) + sizeof(ql_exact::Expm1B))));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
         // one workgroup per frame: the rows' target syndrome bits as sign words
@@ -129,7 +132,7 @@ __device__ __forceinline__ void st_row16(__amdgpu_buffer_rsrc_t rs, int r, doubl
 
 template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
-    if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL);
+    if constexpr (SPLIT) return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL, false, a.split_cb);
     else return V2Layout(a.n, RGLB ? a.rows_lds : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
@@ -147,8 +150,9 @@ __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, in
 #define QL_RL_SPLIT 12
 #endif
 constexpr int V2_RL_SPLIT = QL_RL_SPLIT;
-__host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows) {
-    return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, REG_TSTRIDE, false, true, V2_RL_SPLIT).bytes <= 160 * 1024;
+__host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows, int gcb) {
+    return alg <= 1 &&
+           V2Layout(n, mrows, (n + 3) / 4, REG_TSTRIDE, false, true, V2_RL_SPLIT, false, gcb).bytes <= 160 * 1024;
 }
 
 constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
@@ -747,6 +751,60 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 STAMP(ST_VNK);
                 psync();
                 STAMP(ST_VNK_WAIT);
+            }
+            if constexpr (SPLIT) {
+                if (a.xoff) {
+                    // Exchange gather: this part's bits, chunk by chunk, start at
+                    // the channel LLR in LDS; then for kpos 0, 1, ... the region
+                    // of each kpos is read front to back and every term added at
+                    // its bit (one term per bit and kpos: no two lanes of a
+                    // phase touch one sum), so each bit's sum runs in kpos order
+                    // like std::accumulate (:78); the sums go to the totals.
+                    double *const acc = reinterpret_cast<double *>(smem + L.rows);
+                    const int D = a.dv_max, NC = a.split_nc, CB = a.split_cb;
+                    const __amdgpu_buffer_rsrc_t xb_rs =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)a.xbit, (short)0, 0x7fffffff, 0x00020000);
+                    for (int c = 0; c < NC; ++c) {
+                        const int c0 = bit_lo + c * CB;
+                        const int nb = (bit_hi - c0 < CB) ? bit_hi - c0 : CB;
+                        for (int i = tid; i < nb; i += T) acc[i] = llr_of(c0 + i);
+                        __syncthreads();
+                        for (int kk = 0; kk < D; ++kk) {
+                            const int rid = (rank * NC + c) * D + kk;
+                            const int p0 = __builtin_amdgcn_readfirstlane(a.xoff[rid]);
+                            const int p1 = __builtin_amdgcn_readfirstlane(a.xoff[rid + 1]);
+                            for (int p = p0 + tid; p < p1; p += 4 * T) {
+                                uint32_t lb[4];
+                                double v[4], t[4];
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    const int q = p + j * T;
+                                    lb[j] = 0;
+                                    v[j] = 0.0;
+                                    if (q < p1) {
+                                        lb[j] = __builtin_amdgcn_raw_buffer_load_b16(xb_rs, q * 2, 0, 0);
+                                        v[j] = __builtin_bit_cast(
+                                            double, __builtin_amdgcn_raw_buffer_load_b64(stage_rs, q * 8, 0, 0));
+                                    }
+                                }
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+                                    if (p + j * T < p1) t[j] = acc[lb[j]];
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+                                    if (p + j * T < p1) acc[lb[j]] = t[j] + v[j];
+                            }
+                            __syncthreads();
+                        }
+                        // (the next chunk's LLR store hits the same acc[i] from
+                        // the same thread: no barrier before it)
+                        for (int i = tid; i < nb; i += T) total[c0 + i] = acc[i];
+                    }
+                    STAMP(ST_VNK);
+                    psync();
+                    STAMP(ST_VNK_WAIT);
+                    return;
+                }
             }
             if constexpr (GATHER) {
                 // terms k0 .. dv-1 of each high-degree bit, in order, from the stage
@@ -1377,12 +1435,17 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds) {
-    if (split) return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m) ? V2_RL_SPLIT : 0).bytes;
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds, int gcb) {
+    if (split)
+        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb) ? V2_RL_SPLIT : 0,
+                        false, gcb)
+            .bytes;
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
     return V2Layout(n, rows_lds >= 0 ? rows_lds : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
                     V2_ROWSCAN_ON && !split && RG == 0).bytes;
 }
+
+bool v2_split_rl_fits(int n, int mrows, int gcb) { return v2_use_rl_split(0, n, mrows, gcb); }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
     if (alg < 2 || split_k > 1 || m >= 0xFFFF) return false;
@@ -1405,7 +1468,7 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
-                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows)
+                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb)
                                                      : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);

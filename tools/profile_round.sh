@@ -34,6 +34,7 @@ for wl in ${WLS:-c2 c3}; do
       valu)  pass ${wl}_valu "$B" --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 --kernel-trace ;;
       tcc)   pass ${wl}_tcc "$B" --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace ;;
       ea)    pass ${wl}_ea "$B" --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum --kernel-trace ;;
+      stall) pass ${wl}_stall "$B" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace ;;
       lds)   pass ${wl}_lds "$B" --pmc SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL --kernel-trace ;;
       *) echo "unknown pass $p" >&2; exit 2 ;;
     esac
