@@ -34,6 +34,12 @@ constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS roun
 #ifndef QL_MSG_PF
 #define QL_MSG_PF 1  // stage-writing message passes request the next group's metadata early
 #endif
+#ifndef QL_XG_UNROLL
+#define QL_XG_UNROLL 4  // split exchange gather: terms per thread per load round (8: spills, 10% slower C4)
+#endif
+#ifndef QL_SPLIT_TANH_W
+#define QL_SPLIT_TANH_W 1  // split-frame SPA: tanh's expm1 table in the word form (exact_math.h Expm1Bw)
+#endif
 #ifndef QL_HOIST_LLR
 #define QL_HOIST_LLR 0  // (A/B) SPA message pass: the kpos-0 channel LLR requested first
 #endif
@@ -322,7 +328,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const ql_exact::Expm1Tab ctab{ctab_a, ctab_b, 2};
     if constexpr (ALG == 0) {
         if (tid < ql_exact::EXPM1_CLASSES)
-            ql_exact::expm1_class(tid + ql_exact::EXPM1_K_MIN, &ctab_a[2 * tid], &ctab_b[2 * tid]);
+            ql_exact::expm1_class<SPLIT && QL_SPLIT_TANH_W>(tid + ql_exact::EXPM1_K_MIN, &ctab_a[2 * tid], &ctab_b[2 * tid]);
     }
 #ifdef QL_PHASE_STAMPS
     uint64_t st_acc[NUM_STAMPS];
@@ -764,6 +770,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     const int D = a.dv_max, NC = a.split_nc, CB = a.split_cb;
                     const __amdgpu_buffer_rsrc_t xb_rs =
                         __builtin_amdgcn_make_buffer_rsrc((void *)a.xbit, (short)0, 0x7fffffff, 0x00020000);
+                    constexpr int XU = QL_XG_UNROLL;  // terms per thread per load round
                     for (int c = 0; c < NC; ++c) {
                         const int c0 = bit_lo + c * CB;
                         const int nb = (bit_hi - c0 < CB) ? bit_hi - c0 : CB;
@@ -773,11 +780,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                             const int rid = (rank * NC + c) * D + kk;
                             const int p0 = __builtin_amdgcn_readfirstlane(a.xoff[rid]);
                             const int p1 = __builtin_amdgcn_readfirstlane(a.xoff[rid + 1]);
-                            for (int p = p0 + tid; p < p1; p += 4 * T) {
-                                uint32_t lb[4];
-                                double v[4], t[4];
+                            for (int p = p0 + tid; p < p1; p += XU * T) {
+                                uint32_t lb[XU];
+                                double v[XU], t[XU];
 #pragma unroll
-                                for (int j = 0; j < 4; ++j) {
+                                for (int j = 0; j < XU; ++j) {
                                     const int q = p + j * T;
                                     lb[j] = 0;
                                     v[j] = 0.0;
@@ -788,10 +795,10 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                                     }
                                 }
 #pragma unroll
-                                for (int j = 0; j < 4; ++j)
+                                for (int j = 0; j < XU; ++j)
                                     if (p + j * T < p1) t[j] = acc[lb[j]];
 #pragma unroll
-                                for (int j = 0; j < 4; ++j)
+                                for (int j = 0; j < XU; ++j)
                                     if (p + j * T < p1) acc[lb[j]] = t[j] + v[j];
                             }
                             __syncthreads();
@@ -961,7 +968,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     if constexpr (SPA_FAM) {
                         double t = b;
                         if constexpr (ALG == 0) {
-                            if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // (:60)
+                            if (compute) t = ql_exact::tanh_half_clip_t<SPLIT && QL_SPLIT_TANH_W>(b, lim_it, tlim_it, &div_unsafe, ctab);  // (:60)
                         } else {
                             if (compute) t = tanh_lin(b / 2.);
                         }
@@ -1082,7 +1089,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     // into tanh_half_clip with the iteration's (lim, thr).
                     const double b = tv - c2b.get_seq(k);
                     double t = b;
-                    if (compute) t = ql_exact::tanh_half_clip_t(b, lim_it, tlim_it, &div_unsafe, ctab);  // tanh(b2c / 2.) (:60)
+                    if (compute) t = ql_exact::tanh_half_clip_t<SPLIT && QL_SPLIT_TANH_W>(b, lim_it, tlim_it, &div_unsafe, ctab);  // tanh(b2c / 2.) (:60)
                     c2b.set(k, t);
                     const double st = (s ? -1. : 1.) * t;  // (:57-62)
                     acc = start ? st : acc * t;

@@ -680,12 +680,19 @@ struct alignas(16) Expm1A {
 struct alignas(16) Expm1B {
     double b, c;
 };
+// The word form of the B part (W = true below): B and C as high words and the
+// exponent addend k << 20 stored, not shifted — the form the split-frame SPA
+// instantiation runs faster with (fewer live registers there).
+struct alignas(16) Expm1Bw {
+    uint32_t b_hi, c_hi, k20, pad;
+};
 struct Expm1Tab {
     const Expm1A *a;
     const Expm1B *b;
     int step;  // entry stride in 16-byte units (1: two arrays)
 };
 constexpr int EXPM1_K_MIN = -3, EXPM1_K_MAX = 63, EXPM1_CLASSES = EXPM1_K_MAX - EXPM1_K_MIN + 1;
+template <bool W = false>
 QL_HD void expm1_class(int32_t k, Expm1A *ea, Expm1B *eb) {
     const uint32_t ku = (uint32_t)k;
     const bool fcls = (ku - 20u) <= 36u;
@@ -696,8 +703,16 @@ QL_HD void expm1_class(int32_t k, Expm1A *ea, Expm1B *eb) {
     a_hi = (k == -1) ? 0xbff00000u : a_hi;
     ea->x3 = from_words(fcls ? (0x3ff00000u - (ku << 20)) : 0x80000000u, 0u);
     ea->x4 = from_words(fcls ? 0x3ff00000u : a_hi, 0u);
-    eb->b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
-    eb->c = from_words(big ? 0x3ff00000u : 0x80000000u, 0u);
+    if constexpr (W) {
+        Expm1Bw *ew = reinterpret_cast<Expm1Bw *>(eb);
+        ew->b_hi = far ? 0xbff00000u : 0x80000000u;
+        ew->c_hi = big ? 0x3ff00000u : 0x80000000u;
+        ew->k20 = ku << 20;
+        ew->pad = 0;
+    } else {
+        eb->b = from_words(far ? 0xbff00000u : 0x80000000u, 0u);
+        eb->c = from_words(big ? 0x3ff00000u : 0x80000000u, 0u);
+    }
 }
 
 // tanh_half_common with the class constants from `tab` (EXPM1_CLASSES
@@ -708,6 +723,9 @@ QL_HD void expm1_class(int32_t k, Expm1A *ea, Expm1B *eb) {
 // range, where invln2 * u - 0.5 lies in [-1.99999997, -1.00000001] — so only
 // the k = 0 test (|u| <= 0.5 ln2 by hi word) remains.  The result's sign:
 // the magnitude C + num / (y + 2) is > 0 on this path, so copysign by b.
+// W: the table's B parts are in the word form (expm1_class<true>), and u is
+// the select of +-|b| — the same IEEE operations either way.
+template <bool W = false>
 QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     const double ln2_hi = 6.93147180369123816490e-01;
     const double ln2_lo = 1.90821492927058770002e-10;
@@ -724,7 +742,8 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     // a copy of the low word; |b| is the multiply's abs source modifier)
 #if defined(__HIP_DEVICE_COMPILE__)
     double u;
-    asm("v_mul_f64 %0, |%1|, %2" : "=v"(u) : "v"(b), "v"(big ? 1.0 : -1.0));
+    if constexpr (W) u = big ? __builtin_fabs(b) : -__builtin_fabs(b);
+    else asm("v_mul_f64 %0, |%1|, %2" : "=v"(u) : "v"(b), "v"(big ? 1.0 : -1.0));
 #else
     const double u = big ? __builtin_fabs(b) : -__builtin_fabs(b);
 #endif
@@ -737,6 +756,7 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     const int32_t kc = k < EXPM1_K_MIN ? EXPM1_K_MIN : (k > EXPM1_K_MAX ? EXPM1_K_MAX : k);
     const Expm1A ca = tab.a[(kc - EXPM1_K_MIN) * tab.step];  // issued early, used after the division
     const Expm1B cb = tab.b[(kc - EXPM1_K_MIN) * tab.step];
+    const Expm1Bw cw = reinterpret_cast<const Expm1Bw *>(tab.b)[(kc - EXPM1_K_MIN) * tab.step];
     const double t = (double)k;
     const double hi = __builtin_fma(-t, ln2_hi, u);  // == u - t * ln2_hi: t * ln2_hi is exact (ln2_hi has 32 bits, |k| < 2^11)
     const double lo = t * ln2_lo;
@@ -757,9 +777,10 @@ QL_HD double tanh_half_common_t(double b, uint32_t *ib_out, Expm1Tab tab) {
     // s_tanh.c evaluates |x| and negates last: z = +-(C + num / (y + 2)) with
     // C = 1, num = -2 (|x| >= 1) or C = -0, num = -y; the sign goes on at the
     // end (round-to-nearest is symmetric; the sum is never 0 on this path).
-    const double y = with_hi_word(ypre, hi_word(ypre) + ((uint32_t)kc << 20)) + cb.b;
+    const double y = W ? with_hi_word(ypre, hi_word(ypre) + cw.k20) + from_words(cw.b_hi, 0u)
+                       : with_hi_word(ypre, hi_word(ypre) + ((uint32_t)kc << 20)) + cb.b;
     const double num = big ? from_words(0xc0000000u, 0u) : from_words(hi_word(y) ^ 0x80000000u, lo_word(y));
-    const double zp = cb.c + div_rn_safe(num, y + 2.0);
+    const double zp = (W ? from_words(cw.c_hi, 0u) : cb.c) + div_rn_safe(num, y + 2.0);
     *ib_out = ib;
     return __builtin_copysign(zp, b);
 }
@@ -798,9 +819,10 @@ QL_HD double tanh_half_clip(double b, double lim, double t_lim, int *tiny_or_nan
 }
 
 // tanh_half_clip on tanh_half_common_t (the table form).
+template <bool W = false>
 QL_HD double tanh_half_clip_t(double b, double lim, double t_lim, int *tiny_or_nan, Expm1Tab tab) {
     uint32_t ib;
-    double z = tanh_half_common_t(b, &ib, tab);
+    double z = tanh_half_common_t<W>(b, &ib, tab);
     const bool special = (ib < 0x3c900000u) || !(__builtin_fabs(b) < lim);
     QL_RARE(special) {
         const double x = b / 2.;

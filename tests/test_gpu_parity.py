@@ -339,6 +339,28 @@ def test_c4_generated_dv4_ten_parts(gpu_available, alg, prim, sec):
         assert bits_equal_nan(out.posterior[f], op[f])
 
 
+@pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0)])
+def test_c4_100k_split_term_major_stage(gpu_available, monkeypatch, alg, prim, sec):
+    """QLDPC_SPLIT_X=0 (read when the graph is created): split frames sum their
+    VN terms from the term-major stage instead of the exchange layout (the A/B
+    arm of DecodeArgs::xoff) — same bits, iterations and posteriors as the
+    oracle and as the default graph."""
+    H = load_fixture("c4s_n102400_m32001.alist")
+    monkeypatch.setenv("QLDPC_SPLIT_X", "0")
+    g0 = Q.Graph(H)
+    monkeypatch.delenv("QLDPC_SPLIT_X")
+    _, _, llr, synd = frames(H, 0.038, 6, 90 + alg)
+    p = Q.Params(alg, 10, True, 100.0, prim, sec)
+    out0 = g0.decode(p, llr, synd, posterior=True)
+    out1 = graph("c4s_n102400_m32001.alist").decode(p, llr, synd, posterior=True)
+    O = Oracle(H)
+    ob, oi, ok, op = O.decode_batch(O.params(alg, 10, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
+    for out in (out0, out1):
+        for f in range(llr.shape[0]):
+            assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
+            assert bits_equal_nan(out.posterior[f], op[f])
+
+
 @pytest.mark.parametrize("batch", [1, 2])
 def test_c4_100k_split_few_frames(gpu_available, batch):
     # fewer frames than XCDs: most part groups draw no frame and leave

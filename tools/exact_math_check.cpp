@@ -24,12 +24,16 @@ static thread_local int dummy_flag = 0;
 // the decoder's expm1 class table (exact_math.h: tanh_half_common_t)
 static ql_exact::Expm1A g_ctab_a[ql_exact::EXPM1_CLASSES];
 static ql_exact::Expm1B g_ctab_b[ql_exact::EXPM1_CLASSES];
-static double tanh_t(double b, double lim, double tl) {
-    return ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_b, 1});
-}
+static ql_exact::Expm1B g_ctab_bw[ql_exact::EXPM1_CLASSES];  // the word form (expm1_class<true>)
 static inline bool same(double a, double b) {
     if (a != a && b != b) return true;
     uint64_t x, y; memcpy(&x, &a, 8); memcpy(&y, &b, 8); return x == y;
+}
+// both table forms; a disagreement between them is reported as a mismatch
+static double tanh_t(double b, double lim, double tl) {
+    const double z0 = ql_exact::tanh_half_clip_t(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_b, 1});
+    const double z1 = ql_exact::tanh_half_clip_t<true>(b, lim, tl, &dummy_flag, ql_exact::Expm1Tab{g_ctab_a, g_ctab_bw, 1});
+    return same(z0, z1) ? z0 : -999.0;
 }
 // input generators: mode selects a distribution
 static double gen(uint64_t &s, int mode) {
@@ -47,7 +51,10 @@ int main(int argc, char **argv) {
     uint64_t seed0 = argc > 2 ? strtoull(argv[2], 0, 10) : 12345;
     unsigned nt = std::thread::hardware_concurrency(); if (!nt) nt = 4;
     for (int i = 0; i < ql_exact::EXPM1_CLASSES; ++i)
+    {
         ql_exact::expm1_class(i + ql_exact::EXPM1_K_MIN, &g_ctab_a[i], &g_ctab_b[i]);
+        ql_exact::expm1_class<true>(i + ql_exact::EXPM1_K_MIN, &g_ctab_a[i], &g_ctab_bw[i]);
+    }
     const char *names[15] = {"tanh", "atanh", "expm1", "log1p", "tanh_bf", "atanh_bf", "expm1_bf", "log1p_bf", "tanh_dec", "atanh_dec", "tanh_half_dec", "atanh2_dec", "tanh_half_clip", "atanh2_clip", "tanh_half_clip_t"};
     std::atomic<long> bad[15]; for (auto &b : bad) b = 0;
     std::vector<std::thread> th;

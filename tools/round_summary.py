@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import summarize  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PASSES = ("fetch", "write", "sq", "sq2", "valu", "tcc", "ea", "lds")
+PASSES = ("fetch", "write", "sq", "sq2", "valu", "tcc", "ea", "lds", "stall")
 
 
 def main(prof, tag, rnd="r03"):
