@@ -27,7 +27,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "decoded info-bits/sec (whole node), n=10k R=0.8 SPA 50-iter, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_PEAK_WAVE_INSTR = 5.09e11  # measured: tools/valu_bench.hip, independent v_fma_f64 chains, 256 CUs
+# Highest VALU issue rate measured on MI355X (issue slots/s, whole chip):
+# tools/valu_bench.hip's SPA edge-math loop at 2.30 GHz (profiles/r04/
+# valu_microbench_r04.json).  Dense v_fma_f64 chains reach only 4.4-5.1e11
+# because the chip lowers its clock to 1.95-2.2 GHz on them; the decode
+# kernels run at 2.3 GHz, so that rate understated their peak.
+VALU_PEAK_WAVE_INSTR = 5.73e11
 
 WORKLOADS = {
     # name: matrix fixture, format, algorithm, primary, secondary, qber, batch/GPU, description
@@ -304,8 +309,8 @@ def main():
             # (profiles/pmc_<workload>.json: SQ_ACTIVE_INST_VALU, where a
             # v_rcp_f64 counts 4 like its issue time; SQ_INSTS_VALU if absent)
             # over this run's kernel time, against the whole-chip rate of
-            # full-rate VALU instructions tools/valu_bench.hip measures
-            # (profiles/r01/valu_microbench.json).
+            # VALU issue slots tools/valu_bench.hip measures
+            # (profiles/r04/valu_microbench_r04.json).
             busy = valu_busy or valu_per_launch
             ach = busy / (kms * 1e-3)
             res["compute_roofline"] = {"bound": "fp64-valu-issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INSTR,

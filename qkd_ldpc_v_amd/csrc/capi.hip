@@ -2341,16 +2341,19 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
     if (plan && plan->n_punct + plan->n_short > n) return fail(QLDPC_EINVAL, "rate plan does not fit the graph");
     const double lp = qldpc_log_p(q_acc);  // log((1 - q) / q) by the host C library (:1043)
     const int n_punct = plan ? plan->n_punct : 0;
-    // Frames per chunk: the slot's own buffers within ~512 MiB (QLDPC_TRIAL_CHUNK overrides).
+    // Bytes of one trial in a pipeline slot (keys, frames, results, generator workspace).
     const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 +
                              4 * trials_scratch_words(n, n_err, n_punct, 64) / 64;
     const int G = (int)g->devs.size();
     const int per = (count + G - 1) / G;
-    // Frames per chunk: half a device's slice (>= 1024 frames), so generation of
-    // one chunk overlaps the decode of the other, within ~512 MiB of the slot's
-    // own buffers; QLDPC_TRIAL_CHUNK overrides.
+    // Frames per chunk: a device's whole slice within ~512 MiB of the slot's own
+    // buffers (16384 frames at most); longer slices alternate chunks over the
+    // two slots, so a chunk's trials are generated while the CUs the other's
+    // decode frees in its tail sit idle.  (The persistent decode holds every
+    // CU, so halving a slice buys no overlap: C2, 4096 trials, 2 x 2048 took
+    // 22.3 ms, 1 x 4096 21.5 ms; profiles/r04/seam_chunk_ab.txt.)
+    // QLDPC_TRIAL_CHUNK overrides.
     int cap = (int)std::max<size_t>(1, std::min<size_t>(16384, ((size_t)512 << 20) / per_frame));
-    cap = std::min(cap, std::max(1024, (per + 1) / 2));
     if (env_int("QLDPC_TRIAL_CHUNK", 0) > 0) cap = env_int("QLDPC_TRIAL_CHUNK", 0);
     std::vector<int> rcs(G, QLDPC_OK);
     std::vector<std::string> errs(G);

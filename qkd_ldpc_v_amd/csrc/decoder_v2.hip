@@ -376,11 +376,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // instead of VGPRs with waterfall loops around each access
         const int f = __builtin_amdgcn_readfirstlane(*s_frame);
         if (f >= a.batch) break;
-        // the trial's own span inside the batch starts at its claim (a.frame_clk)
-        uint64_t clk0 = 0;
-        if (tid == 0 && a.frame_clk) clk0 = __builtin_amdgcn_s_memrealtime();
         // SPLIT: this part's lanes, waves, metadata and rows; the group barrier
         const int rank = SPLIT ? __builtin_amdgcn_readfirstlane(s_part[0]) : 0;
+        // the trial's own span inside the batch starts at its claim
+        // (a.frame_clk; stored now, so no register holds it through the decode)
+        if (tid == 0 && rank == 0 && a.frame_clk) a.frame_clk[2 * (size_t)f] = __builtin_amdgcn_s_memrealtime();
         const int tg = SPLIT ? rank * REG_TSTRIDE + tid : tid;
         const int head_in = SPLIT ? a.lane_head[tg] : head_in0;
         const int row0_in = SPLIT ? a.lane_row0[tg] : row0_in0;
@@ -1314,10 +1314,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         if (tid == 0 && rank == 0) {
             a.iters[f] = (uint32_t)iters;
             a.ok[f] = (uint8_t)okv;
-            if (a.frame_clk) {
-                a.frame_clk[2 * (size_t)f] = clk0;
-                a.frame_clk[2 * (size_t)f + 1] = __builtin_amdgcn_s_memrealtime();
-            }
+            if (a.frame_clk) a.frame_clk[2 * (size_t)f + 1] = __builtin_amdgcn_s_memrealtime();
         }
         STAMP(ST_OUT);
         __syncthreads();
