@@ -1068,20 +1068,36 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         if (fill[NR] != g->stage_doubles) return fail(QLDPC_EUNSUP, "split exchange layout: term count");
         xoff.assign(fill.begin(), fill.end());
         fill.pop_back();
+        // Order inside a region: (writer part, slot group of four, wave, slot,
+        // lane) — the 16 waves of a part, which run the message pass roughly
+        // in step, fill one run per region and slot group together, so a
+        // region has one or two open L2 lines per part instead of one per
+        // wave.  QLDPC_SPLIT_XORDER=0: (wave, slot, lane), one run per wave (A/B).
+        const bool grouped = env_int("QLDPC_SPLIT_XORDER", 1) != 0;
+        const int WPp = REG_TSTRIDE / 64;  // waves per part
         auto assign = [&](const std::vector<uint32_t> &mt, std::vector<uint32_t> &mt2, std::vector<uint16_t> &xb) {
             std::vector<long long> pos(fill);
             xb.assign((size_t)g->stage_doubles, 0);
-            for (int w = 0; w < W; ++w)
-                for (int k = 0; k < S4; ++k)
-                    for (int li = 0; li < 64; ++li) {
-                        const size_t i = midx(w * 64 + li, k);
-                        const uint32_t kp = (mt[i] >> META_KPOS_SHIFT) & META_KPOS_MASK;
-                        if (kp == META_KPOS_MASK) continue;  // dummy slot
-                        const int b = (int)(mt[i] & META_COL_MASK);
-                        const long long q = pos[(size_t)reg0[b] + kp]++;
-                        mt2[i] = (uint32_t)q;
-                        xb[(size_t)q] = (uint16_t)lbit[b];
-                    }
+            auto place = [&](int w, int k) {
+                for (int li = 0; li < 64; ++li) {
+                    const size_t i = midx(w * 64 + li, k);
+                    const uint32_t kp = (mt[i] >> META_KPOS_SHIFT) & META_KPOS_MASK;
+                    if (kp == META_KPOS_MASK) continue;  // dummy slot
+                    const int b = (int)(mt[i] & META_COL_MASK);
+                    const long long q = pos[(size_t)reg0[b] + kp]++;
+                    mt2[i] = (uint32_t)q;
+                    xb[(size_t)q] = (uint16_t)lbit[b];
+                }
+            };
+            if (grouped) {
+                for (int p = 0; p < K; ++p)
+                    for (int k0 = 0; k0 < S4; k0 += 4)
+                        for (int w = p * WPp; w < std::min(W, (p + 1) * WPp); ++w)
+                            for (int k = k0; k < k0 + 4; ++k) place(w, k);
+            } else {
+                for (int w = 0; w < W; ++w)
+                    for (int k = 0; k < S4; ++k) place(w, k);
+            }
         };
         assign(meta, meta2, xbit);
         assign(meta_ms, meta2_ms, xbit_ms);
