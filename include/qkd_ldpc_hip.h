@@ -244,6 +244,11 @@ int qldpc_device_count(int32_t *count);
  * the accurate QBER floor(n*qber)/n; QLDPC_EINVAL (the reference's "too small
  * for QBER" error) when floor(n*qber) == 0. */
 int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_out);
+/* qldpc_xoshiro_jump: the Xoshiro256 state (s0..s3) of a generator seeded
+ * like Xoshiro-cpp with `seed`, after `draws` draws, by the GF(2) jump matrix
+ * the device trial generator starts its second wave from (draws = n: the state
+ * after fill_random_bits).  Host only; the generator's self-check. */
+int qldpc_xoshiro_jump(uint64_t seed, uint64_t draws, uint64_t *state_out);
 int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
                         uint8_t *d_alice, uint8_t *d_bob, double *accurate_qber_out, void *stream);
 

@@ -80,6 +80,7 @@ _SIGNATURES = {
     ),
     "qldpc_selftest_math_device": (_I32, [_I32, _I32, _P, _P, _P]),
     "qldpc_trial_seeds": (_I32, [ctypes.c_uint64, _I32, _P]),
+    "qldpc_xoshiro_jump": (_I32, [ctypes.c_uint64, ctypes.c_uint64, _P]),
     "qldpc_xoshiro_state": (_I32, [ctypes.c_uint64, _P]),
     "qldpc_sort_permutation": (_I32, [_P, _I32, _P]),
     "qldpc_bits_to_remove": (_I32, [_I32, _I32, _P, _P, _I32, _P, _I32, _P, _I32, _P, _PI32]),

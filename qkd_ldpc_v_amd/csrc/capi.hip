@@ -2312,6 +2312,11 @@ int qldpc_trial_seeds(uint64_t simulation_seed, int32_t count, uint64_t *seeds_o
     return QLDPC_OK;
 }
 
+int qldpc_xoshiro_jump(uint64_t seed, uint64_t draws, uint64_t *state_out) {
+    if (!state_out) return fail(QLDPC_EINVAL, "NULL state_out");
+    return xoshiro_jump_check(seed, draws, state_out);
+}
+
 int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
                         uint8_t *d_alice, uint8_t *d_bob, double *accurate_qber_out, void *stream) {
     if (n <= 0 || batch < 0) return fail(QLDPC_EINVAL, "n must be > 0 and batch >= 0");

@@ -216,6 +216,9 @@ hipError_t launch_palettize(int n, int nc, int batch, const double *llr, uint8_t
                             uint8_t *pal_ok, const int32_t *col_orig, hipStream_t stream);
 // Trial generator workspace (uint32 words) of `batch` trials.
 size_t trials_scratch_words(int n, uint64_t n_err, int n_punct, int batch);
+// The Xoshiro256 state after `draws` draws from a Xoshiro-cpp-seeded generator,
+// by the jump matrix the trial generator's second wave uses (host; a check).
+int xoshiro_jump_check(uint64_t seed, uint64_t draws, uint64_t *state_out);
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream);

@@ -37,6 +37,9 @@ constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS roun
 #ifndef QL_XG_UNROLL
 #define QL_XG_UNROLL 4  // split exchange gather: terms per thread per load round (8: spills, 10% slower C4)
 #endif
+#ifndef QL_GH_PF
+#define QL_GH_PF 1  // hybrid bit gather: the next bit's entry requested one bit ahead
+#endif
 #ifndef QL_SPLIT_TANH_W
 #define QL_SPLIT_TANH_W 1  // split-frame SPA: tanh's expm1 table in the word form (exact_math.h Expm1Bw)
 #endif
@@ -661,13 +664,18 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                         const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 0));
                         return make_uint2(v.x, v.y);
                     };
+                    // the next bit's entry is requested one bit ahead (its rows
+                    // and their aggregates then wait one load each, not two)
+                    uint2 e_n = make_uint2(0u, 0u);
+                    if (tid < n) e_n = ld2(vb_rs, (uint32_t)tid * 8u);
                     for (int i = tid; i < n; i += T) {
-                        const uint2 e = ld2(vb_rs, (uint32_t)i * 8u);
+                        const uint2 e = QL_GH_PF ? e_n : ld2(vb_rs, (uint32_t)i * 8u);
                         const int b = (int)e.x;
                         const uint32_t c0 = e.y & 0xFFFFFFu;
                         const int dvb = (int)(e.y >> 24);
-                        double sacc = llr_of(b);
                         uint2 rr = ld2(vr_rs, c0 * 8u);
+                        if (QL_GH_PF && i + T < n) e_n = ld2(vb_rs, (uint32_t)(i + T) * 8u);
+                        double sacc = llr_of(b);
                         for (int kc = 0; kc < dvb; kc += 4) {
                             const uint32_t ch = c0 + (uint32_t)(kc >> 2);
                             const uint2 cur = rr;

@@ -25,8 +25,21 @@
 // 256-byte line); a second kernel expands them into the byte keys, one
 // workgroup per trial.  The same draws are consumed in the same order, so the
 // keys are the reference's bit for bit.
+//
+// Two waves per 64 trials: Alice's n draws and the rest of the chain are two
+// independent stretches of one generator stream, and Xoshiro256's state
+// transition is linear over GF(2), so the state at draw n is J_n · s with the
+// 256 x 256 bit matrix J_n = M^n (built on the host once per n).  One wave
+// draws Alice's bits from s, the other starts at J_n · s and runs the shuffle
+// and the punctured draws: the same draws in the same order, in parallel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
 
 namespace qldpc {
 namespace {
@@ -89,24 +102,49 @@ struct TrialWs {
     __host__ __device__ size_t pbob() const { return 2 * (size_t)words + (size_t)k + (size_t)pwords; }
 };
 
+// jump: J_n as 256 columns of four words (nullptr: one wave runs the whole
+// chain); the grid then has two waves per 64 trials, Alice's bits in the first
+// half of the blocks, the rest of the chain in the second.
 __global__ void __launch_bounds__(64) trials_lanes_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
-                                                          uint64_t seed_add, uint32_t *ws, int n_punct) {
+                                                          uint64_t seed_add, uint32_t *ws, int n_punct,
+                                                          const uint64_t *__restrict__ jump) {
     const int lane = threadIdx.x;
-    const int f = blockIdx.x * 64 + lane;
+    const int nblk = (batch + 63) / 64;
+    const bool split = jump != nullptr;
+    const bool tail = split && (int)blockIdx.x >= nblk;  // this wave starts at draw n
+    const int blk = tail ? (int)blockIdx.x - nblk : (int)blockIdx.x;
+    const int f = blk * 64 + lane;
     const TrialWs L(n, n_err, n_punct);
     // this wave's 64 columns, [word][lane]
-    uint32_t *col = ws + (size_t)blockIdx.x * L.per_lane() * 64 + lane;
+    uint32_t *col = ws + (size_t)blk * L.per_lane() * 64 + lane;
     auto at = [&](size_t word) -> uint32_t & { return col[word * 64]; };
     Xoshiro256pp g((f < batch ? seeds[f] : 0ull) + seed_add);
-    // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
-    // which never rejects: the top bit of each draw.
-    for (int w = 0; w < L.words; ++w) {
-        uint32_t v = 0;
-        const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
-        for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
-        at(L.abits() + w) = v;
-        at(L.flips() + w) = 0u;
+    if (!tail) {
+        // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
+        // which never rejects: the top bit of each draw.
+        for (int w = 0; w < L.words; ++w) {
+            uint32_t v = 0;
+            const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
+            for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
+            at(L.abits() + w) = v;
+        }
+        if (split) return;
+    } else {
+        // the state after Alice's n draws: J_n · s over GF(2) (columns by
+        // wave-uniform loads)
+        const uint64_t s[4] = {g.s0, g.s1, g.s2, g.s3};
+        uint64_t r[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 256; ++j) {
+            const uint64_t m = 0ull - ((s[j >> 6] >> (j & 63)) & 1ull);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) r[q] ^= jump[4 * j + q] & m;
+        }
+        g.s0 = r[0];
+        g.s1 = r[1];
+        g.s2 = r[2];
+        g.s3 = r[3];
     }
+    for (int w = 0; w < L.words; ++w) at(L.flips() + w) = 0u;
     const uint32_t k = (uint32_t)n_err;
     if (k > 0) {
         for (uint32_t e = 0; e < k; ++e) at(L.perm() + e) = e;
@@ -262,6 +300,92 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
     return hipGetLastError();
 }
 
+namespace {
+
+// J_d = M^d for Xoshiro256's state transition M, column-major: column j (four
+// words) is J_d applied to the unit state e_j.  Host code, once per d.
+void xo_step(uint64_t s[4]) {
+    const uint64_t t = s[1] << 17;
+    s[2] ^= s[0];
+    s[3] ^= s[1];
+    s[1] ^= s[2];
+    s[0] ^= s[3];
+    s[2] ^= t;
+    s[3] = (s[3] << 45) | (s[3] >> 19);
+}
+void gf2_mul(const uint64_t *A, const uint64_t *B, uint64_t *C) {  // C = A B (256 x 256, columns)
+    for (int j = 0; j < 256; ++j) {
+        uint64_t r[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 256; ++i)
+            if ((B[4 * j + (i >> 6)] >> (i & 63)) & 1ull)
+                for (int q = 0; q < 4; ++q) r[q] ^= A[4 * i + q];
+        std::memcpy(C + 4 * j, r, sizeof r);
+    }
+}
+void xo_jump_matrix(uint64_t d, uint64_t *J) {
+    uint64_t M[1024], P[1024], T[1024];  // (24 KiB of host stack; no shared state)
+    for (int j = 0; j < 256; ++j) {
+        uint64_t s[4] = {0, 0, 0, 0};
+        s[j >> 6] = 1ull << (j & 63);
+        xo_step(s);
+        std::memcpy(M + 4 * j, s, sizeof s);
+    }
+    std::memset(J, 0, 1024 * sizeof(uint64_t));
+    for (int j = 0; j < 256; ++j) J[4 * j + (j >> 6)] = 1ull << (j & 63);
+    std::memcpy(P, M, sizeof M);
+    for (; d; d >>= 1) {  // powers of M commute: the product order is free
+        if (d & 1) {
+            gf2_mul(P, J, T);
+            std::memcpy(J, T, sizeof T);
+        }
+        if (d > 1) {
+            gf2_mul(P, P, T);
+            std::memcpy(P, T, sizeof T);
+        }
+    }
+}
+// J_n on a device, built and uploaded once per (device, n) for the process.
+std::mutex g_jump_mu;
+std::map<std::pair<int, int>, uint64_t *> g_jump;
+hipError_t jump_on_device(int n, const uint64_t **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_jump_mu);
+    auto it = g_jump.find({dev, n});
+    if (it == g_jump.end()) {
+        uint64_t J[1024];
+        xo_jump_matrix((uint64_t)n, J);
+        uint64_t *d = nullptr;
+        if ((e = hipMalloc(&d, sizeof J)) != hipSuccess) return e;
+        if ((e = hipMemcpy(d, J, sizeof J, hipMemcpyHostToDevice)) != hipSuccess) {
+            (void)hipFree(d);
+            return e;
+        }
+        it = g_jump.emplace(std::make_pair(dev, n), d).first;
+    }
+    *out = it->second;
+    return hipSuccess;
+}
+
+}  // namespace
+
+int xoshiro_jump_check(uint64_t seed, uint64_t d, uint64_t *state_out) {
+    uint64_t J[1024], s[4], x = seed;
+    for (auto &v : s) {  // Xoshiro-cpp seeding (four SplitMix64 outputs)
+        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        v = z ^ (z >> 31);
+    }
+    xo_jump_matrix(d, J);
+    for (int q = 0; q < 4; ++q) state_out[q] = 0;
+    for (int j = 0; j < 256; ++j)
+        if ((s[j >> 6] >> (j & 63)) & 1ull)
+            for (int q = 0; q < 4; ++q) state_out[q] ^= J[4 * j + q];
+    return 0;
+}
+
 size_t trials_scratch_words(int n, uint64_t n_err, int n_punct, int batch) {
     return TrialWs(n, n_err, n_punct).per_lane() * 64 * (size_t)((batch + 63) / 64);
 }
@@ -271,8 +395,16 @@ hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds
                          hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     if (!scratch) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(trials_lanes_kernel, dim3((batch + 63) / 64), dim3(64), 0, stream, n, n_err, batch, seeds,
-                       seed_add, scratch, n_punct);
+    // two waves per 64 trials (QLDPC_TRIAL_SPLIT=0: one, A/B)
+    const uint64_t *jump = nullptr;
+    const char *env = std::getenv("QLDPC_TRIAL_SPLIT");
+    if (!(env && std::strcmp(env, "0") == 0)) {
+        hipError_t je = jump_on_device(n, &jump);
+        if (je != hipSuccess) return je;
+    }
+    const int nblk = (batch + 63) / 64;
+    hipLaunchKernelGGL(trials_lanes_kernel, dim3(jump ? 2 * nblk : nblk), dim3(64), 0, stream, n, n_err, batch,
+                       seeds, seed_add, scratch, n_punct, jump);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(trials_expand_kernel, dim3(batch), dim3(256), 0, stream, n, n_err, batch, scratch, alice, bob,

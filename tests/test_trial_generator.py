@@ -127,6 +127,18 @@ def test_oracle_trial_matches_python_restatement(n, qber, seed):
     assert int((a != b).sum()) == int(n * qber)
 
 
+@pytest.mark.parametrize("seed,draws", [(1, 0), (1, 1), (9012025, 1024), (1022025, 10240), (2**64 - 7, 102400)])
+def test_xoshiro_jump_matrix(seed, draws):
+    """The device generator's second wave starts from J_n . s (GF(2) jump,
+    trials.hip): the host jump equals stepping the generator `draws` times."""
+    g = PyXoshiro(seed)
+    for _ in range(draws):
+        g()
+    out = np.zeros(4, np.uint64)
+    Q._lib.check(Q.lib().qldpc_xoshiro_jump(seed, draws, out.ctypes.data), "qldpc_xoshiro_jump")
+    assert [int(v) for v in out] == g.s
+
+
 def test_seed_sequences_agree():
     g = PyXoshiro(1022025)
     want = np.array([g() for _ in range(16)], np.uint64)
