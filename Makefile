@@ -16,6 +16,10 @@ CSRC := $(PKG)/csrc
 # without it; tests/test_capi.py checks the flag is on every product compile line.
 HIPFLAGS := --offload-arch=$(ARCH) $(EXTRA_HIPFLAGS) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-result \
             -mllvm -amdgpu-atomic-optimizer-strategy=None
+# The decoder kernels are scheduled with LLVM's iterative ILP strategy: same
+# instructions and bits, 0.6% (C2) / 1.4% (C5) / 2.3% (C4) shorter decode
+# in a same-box A/B against the default strategy (profiles/r04/sched_strategy_ab.txt).
+V2FLAGS := -mllvm --amdgpu-sched-strategy=iterative-ilp
 LIB := $(PKG)/libqkdldpc_hip.so
 ORACLE := oracle/libqkdldpc_oracle.so
 HOSTCHK := $(PKG)/host/host_mirror_check
@@ -27,8 +31,8 @@ all: $(LIB) $(ORACLE) $(HOSTCHK) $(DROPIN) $(BATCHCHK)
 $(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h Makefile
+	$(HIPCC) $(HIPFLAGS) $(V2FLAGS) -c $< -o $@
 
 $(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -54,7 +58,7 @@ stamps: $(STAMPLIB)
 $(CSRC)/decoder_st.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/decoder_v2_st.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h
-	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(V2FLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(CSRC)/capi_st.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp $(CSRC)/relabel.hpp include/qkd_ldpc_hip.h
 	$(HIPCC) $(HIPFLAGS) -DQL_PHASE_STAMPS -c $< -o $@
 $(STAMPLIB): $(CSRC)/decoder_st.o $(CSRC)/decoder_v2_st.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi_st.o $(CSRC)/loaders.o $(CSRC)/relabel.o
@@ -142,6 +146,6 @@ asan-check: asan
 AB ?= x
 ab:
 	mkdir -p $(PKG)/ab/$(AB)
-	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/decoder_v2.hip -o $(PKG)/ab/$(AB)/decoder_v2.o
+	$(HIPCC) $(HIPFLAGS) $(V2FLAGS) $(AB_FLAGS) -c $(CSRC)/decoder_v2.hip -o $(PKG)/ab/$(AB)/decoder_v2.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi.o $(CSRC)/loaders.o $(CSRC)/relabel.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
 .PHONY: ab

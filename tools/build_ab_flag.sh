@@ -7,7 +7,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd "$ROOT"
 HIPFLAGS=$(make -s -f Makefile -f - print-hipflags <<'MK'
 print-hipflags:
-	@echo $(HIPFLAGS)
+	@echo $(HIPFLAGS) $(V2FLAGS)
 MK
 )
 C=qkd_ldpc_v_amd/csrc
