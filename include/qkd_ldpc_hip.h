@@ -346,6 +346,25 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                      int32_t count, const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out,
                      uint8_t *synd_ok_out, uint8_t *keys_match_out, double *runtime_us_out,
                      double *accurate_qber_out);
+/* qldpc_run_trials in two halves, so the simulation loop can put combination
+ * c + 1 on the devices before it collects combination c (the loop over
+ * combinations, src/simulation.cpp:725-765): _submit checks the arguments
+ * exactly as qldpc_run_trials, copies the seeds and enqueues the trials
+ * (blocking only when both of a device's pipeline slots still hold chunks, which
+ * it then collects for their own jobs), and returns a job; _wait completes the
+ * job's outputs, frees it and returns the first error of any device slice.
+ * Between the two the output arrays, the graph and the plan must stay alive;
+ * the seeds need not.  Every submitted job must be waited for. */
+typedef struct qldpc_trials_job qldpc_trials_job;
+int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber,
+                            int32_t count, const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out,
+                            uint8_t *synd_ok_out, uint8_t *keys_match_out, double *runtime_us_out,
+                            double *accurate_qber_out, qldpc_trials_job **job_out);
+int qldpc_run_trials_wait(qldpc_trials_job *job);
+/* The device slice of the batch seam: trials [*lo, *hi) of `count` for shard
+ * `shard` of `shards` (contiguous slices of ceil(count / shards); trailing
+ * shards may be short or empty).  Host only. */
+int qldpc_shard_range(int32_t count, int32_t shards, int32_t shard, int32_t *lo, int32_t *hi);
 
 #ifdef __cplusplus
 }

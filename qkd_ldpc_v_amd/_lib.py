@@ -98,6 +98,11 @@ _SIGNATURES = {
                                    ctypes.POINTER(ctypes.c_double), _P]),
     "qldpc_run_trials": (_I32, [_P, _P, ctypes.POINTER(qldpc_params), ctypes.c_double, _I32, _P, ctypes.c_uint64,
                                 _P, _P, _P, _P, ctypes.POINTER(ctypes.c_double)]),
+    "qldpc_run_trials_submit": (_I32, [_P, _P, ctypes.POINTER(qldpc_params), ctypes.c_double, _I32, _P,
+                                       ctypes.c_uint64, _P, _P, _P, _P, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(_P)]),
+    "qldpc_run_trials_wait": (_I32, [_P]),
+    "qldpc_shard_range": (_I32, [_I32, _I32, _I32, _PI32, _PI32]),
     "qldpc_device_count": (_I32, [_PI32]),
     "qldpc_last_error": (ctypes.c_char_p, []),
     "qldpc_version": (ctypes.c_char_p, []),

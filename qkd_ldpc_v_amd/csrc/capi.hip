@@ -103,6 +103,7 @@ struct TrialSlot {
     double *h_logp = nullptr;
     size_t cap = 0, cap_punct = 0, tscratch_words = 0;
     int f0 = 0, nb = 0;  // the chunk in flight (nb == 0: none)
+    qldpc_trials_job *owner = nullptr;  // the job whose results it holds
 };
 
 struct DeviceGraph {
@@ -138,8 +139,9 @@ struct DeviceGraph {
     std::map<void *, Workspace> ws;
     std::mutex io_mu;  // the host-buffer entry's staging buffers and stream, held copy-in .. copy-out
     HostIO io;
-    std::mutex trial_mu;  // qldpc_run_trials' pipeline slots, held for a whole call
+    std::mutex trial_mu;  // qldpc_run_trials' pipeline slots: held while a job enqueues or harvests
     TrialSlot tslot[2];
+    int next_slot = 0;    // the slot the next chunk takes (the two alternate)
     int occ[6] = {0, 0, 0, 0, 0, 0};
 };
 
@@ -2254,6 +2256,32 @@ void qldpc_rate_plan_destroy(qldpc_rate_plan *plan) {
     delete plan;
 }
 
+namespace {
+// The generator workspace of the _device entries, one per (device, stream),
+// kept across calls so a stream-pipelined caller's launches stay asynchronous
+// (grown, never shrunk; growing drains the device before freeing the old one).
+std::mutex g_tws_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<uint32_t *, size_t>> g_tws;
+hipError_t trial_workspace(hipStream_t s, size_t words, uint32_t **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_tws_mu);
+    auto &w = g_tws[{dev, s}];
+    if (w.second < words) {
+        if (w.first) {
+            if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+            (void)hipFree(w.first);
+            w = {nullptr, 0};
+        }
+        if ((e = hipMalloc(&w.first, std::max<size_t>(words, 1) * sizeof(uint32_t))) != hipSuccess) return e;
+        w.second = words;
+    }
+    *out = w.first;
+    return hipSuccess;
+}
+}  // namespace
+
 int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const uint64_t *d_seeds, uint64_t seed_add,
                                    int32_t n_punct, uint8_t *d_alice, uint8_t *d_bob, uint8_t *d_punct_alice,
                                    uint8_t *d_punct_bob, double *accurate_qber_out, void *stream) {
@@ -2268,14 +2296,9 @@ int qldpc_trials_rate_adapt_device(int32_t n, double qber, int32_t batch, const 
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, n_err, n_punct, batch);
-    if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
+    HIP_TRY(trial_workspace(s, trials_scratch_words(n, n_err, n_punct, batch), &scratch));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, n_punct, d_punct_alice,
                                  d_punct_bob, s);
-    if (scratch) {
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(scratch);
-    }
     if (e != hipSuccess) return hip_fail(e, "trials_rate_adapt");
     return QLDPC_OK;
 }
@@ -2421,22 +2444,85 @@ int qldpc_trials_device(int32_t n, double qber, int32_t batch, const uint64_t *d
     if (!d_seeds || !d_alice || !d_bob) return fail(QLDPC_EINVAL, "NULL device buffer");
     const hipStream_t s = (hipStream_t)stream;
     uint32_t *scratch = nullptr;
-    const size_t words = trials_scratch_words(n, n_err, 0, batch);
-    if (words) HIP_TRY(hipMalloc(&scratch, words * sizeof(uint32_t)));
+    HIP_TRY(trial_workspace(s, trials_scratch_words(n, n_err, 0, batch), &scratch));
     hipError_t e = launch_trials(n, n_err, batch, d_seeds, seed_add, d_alice, d_bob, scratch, 0, nullptr, nullptr, s);
-    if (scratch) {
-        (void)hipStreamSynchronize(s);
-        (void)hipFree(scratch);
-    }
     if (e != hipSuccess) return hip_fail(e, "trials");
     return QLDPC_OK;
 }
 
 
 // ---- the batch seam of the simulation loop (src/simulation.cpp:721-746) ------
-int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber, int32_t count,
-                     const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out, uint8_t *synd_ok_out,
-                     uint8_t *keys_match_out, double *runtime_us_out, double *accurate_qber_out) {
+int qldpc_shard_range(int32_t count, int32_t shards, int32_t shard, int32_t *lo, int32_t *hi) {
+    if (count < 0 || shards <= 0 || shard < 0 || shard >= shards || !lo || !hi)
+        return fail(QLDPC_EINVAL, "bad count / shards / shard / NULL bounds");
+    // contiguous slices of ceil(count / shards); trailing shards may be short or empty
+    const int64_t per = ((int64_t)count + shards - 1) / shards;
+    *lo = (int32_t)std::min<int64_t>(count, (int64_t)shard * per);
+    *hi = (int32_t)std::min<int64_t>(count, (int64_t)*lo + per);
+    return QLDPC_OK;
+}
+
+// One combination's trials in flight: where its results go, and the first
+// error of each device's slice.  Its chunks sit in the devices' pipeline slots
+// (TrialSlot::owner) until harvested — by qldpc_run_trials_wait, or by a later
+// submit that needs the slot.
+struct qldpc_trials_job {
+    qldpc_graph *g = nullptr;
+    uint32_t *iters_out = nullptr;
+    uint8_t *synd_ok_out = nullptr, *keys_match_out = nullptr;
+    double *runtime_us_out = nullptr;
+    std::vector<int> rcs;           // per device slice (written under that device's trial_mu)
+    std::vector<std::string> errs;
+};
+
+namespace {
+
+// Wait for a slot's chunk and deliver its results to the job that owns it:
+// per trial {iterations, syndromes_match, keys_match} and its share of the
+// chunk's window (QKD_LDPC's per-trial window on device, HIP events on the
+// slot's stream) in proportion to its own decode span.  dg->trial_mu held.
+int harvest_slot(qldpc_graph *g, DeviceGraph *dg, int gi, TrialSlot &t) {
+    if (t.nb == 0) return QLDPC_OK;
+    qldpc_trials_job *job = t.owner;
+    const int nb = t.nb;
+    t.nb = 0;
+    t.owner = nullptr;
+    auto body = [&]() -> int {
+        HIP_TRY(hipStreamSynchronize(t.stream));
+        int r = split_check(g, dg, t.stream);
+        if (r) return r;
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, t.ev0, t.ev1));
+        double span_sum = 0.;
+        for (int i = 0; i < nb; ++i) span_sum += (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
+        for (int i = 0; i < nb; ++i) {
+            job->iters_out[t.f0 + i] = t.h_iters[i];
+            job->synd_ok_out[t.f0 + i] = t.h_ok[i];
+            job->keys_match_out[t.f0 + i] = t.h_km[i];
+            if (job->runtime_us_out) {
+                const double span = (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
+                job->runtime_us_out[t.f0 + i] =
+                    span_sum > 0. ? 1e3 * (double)ms * span / span_sum : 1e3 * (double)ms / nb;
+            }
+        }
+        return QLDPC_OK;
+    };
+    const int r = body();
+    if (r && job->rcs[gi] == QLDPC_OK) {  // the error belongs to the owning job's slice
+        job->rcs[gi] = r;
+        job->errs[gi] = g_last_error;
+    }
+    return r;
+}
+
+}  // namespace
+
+int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber,
+                            int32_t count, const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out,
+                            uint8_t *synd_ok_out, uint8_t *keys_match_out, double *runtime_us_out,
+                            double *accurate_qber_out, qldpc_trials_job **job_out) {
+    if (!job_out) return fail(QLDPC_EINVAL, "job_out is NULL");
+    *job_out = nullptr;
     if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
     int rc = check_params(p);
     if (rc) return rc;
@@ -2449,60 +2535,43 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
     if (n_err > (uint64_t)n) return fail(QLDPC_EINVAL, "QBER must be <= 1");
     const double q_acc = (double)n_err / (double)n;  // inject_errors' return (:922-933)
     if (accurate_qber_out) *accurate_qber_out = q_acc;
-    if (count == 0) return QLDPC_OK;
-    if (!seeds || !iters_out || !synd_ok_out || !keys_match_out) return fail(QLDPC_EINVAL, "NULL host buffer");
+    if (count > 0 && (!seeds || !iters_out || !synd_ok_out || !keys_match_out))
+        return fail(QLDPC_EINVAL, "NULL host buffer");
     if (plan && plan->n_punct + plan->n_short > n) return fail(QLDPC_EINVAL, "rate plan does not fit the graph");
+    const int G = (int)g->devs.size();
+    std::unique_ptr<qldpc_trials_job> job(new qldpc_trials_job);
+    job->g = g;
+    job->iters_out = iters_out;
+    job->synd_ok_out = synd_ok_out;
+    job->keys_match_out = keys_match_out;
+    job->runtime_us_out = runtime_us_out;
+    job->rcs.assign(G, QLDPC_OK);
+    job->errs.assign(G, std::string());
+    if (count == 0) {
+        *job_out = job.release();
+        return QLDPC_OK;
+    }
     const double lp = qldpc_log_p(q_acc);  // log((1 - q) / q) by the host C library (:1043)
     const int n_punct = plan ? plan->n_punct : 0;
     // Bytes of one trial in a pipeline slot (keys, frames, results, generator workspace).
     const size_t per_frame = 4 * (size_t)n + (size_t)g->m + 2 * (size_t)n_punct + 64 +
                              4 * trials_scratch_words(n, n_err, n_punct, 64) / 64;
-    const int G = (int)g->devs.size();
-    const int per = (count + G - 1) / G;
     // Frames per chunk: a device's whole slice within ~512 MiB of the slot's own
     // buffers (16384 frames at most); longer slices alternate chunks over the
-    // two slots, so a chunk's trials are generated while the CUs the other's
-    // decode frees in its tail sit idle.  (The persistent decode holds every
-    // CU, so halving a slice buys no overlap: C2, 4096 trials, 2 x 2048 took
-    // 22.3 ms, 1 x 4096 21.5 ms; profiles/r04/seam_chunk_ab.txt.)
-    // QLDPC_TRIAL_CHUNK overrides.
+    // two slots.  (The persistent decode holds every CU, so halving a slice buys
+    // no overlap: C2, 4096 trials, 2 x 2048 took 22.3 ms, 1 x 4096 21.5 ms;
+    // profiles/r04/seam_chunk_ab.txt.)  QLDPC_TRIAL_CHUNK overrides.
     int cap = (int)std::max<size_t>(1, std::min<size_t>(16384, ((size_t)512 << 20) / per_frame));
     if (env_int("QLDPC_TRIAL_CHUNK", 0) > 0) cap = env_int("QLDPC_TRIAL_CHUNK", 0);
-    std::vector<int> rcs(G, QLDPC_OK);
-    std::vector<std::string> errs(G);
+    qldpc_trials_job *J = job.get();
     auto work = [&](int gi) {
         DeviceGraph *dg = g->devs[gi].get();
-        const int lo = std::min(count, gi * per), hi = std::min(count, lo + per);
+        int32_t lo = 0, hi = 0;
+        (void)qldpc_shard_range(count, G, gi, &lo, &hi);
         if (hi <= lo) return;
         auto body = [&]() -> int {
             HIP_TRY(hipSetDevice(dg->device));
             std::lock_guard<std::mutex> lk(dg->trial_mu);
-            // results of a slot's chunk: wait for it, then each trial's share of
-            // the chunk's window (QKD_LDPC's per-trial window on device, HIP
-            // events on its stream) in proportion to its own decode span
-            auto harvest = [&](TrialSlot &t) -> int {
-                if (t.nb == 0) return QLDPC_OK;
-                const int nb = t.nb;
-                t.nb = 0;
-                HIP_TRY(hipStreamSynchronize(t.stream));
-                int r = split_check(g, dg, t.stream);
-                if (r) return r;
-                float ms = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms, t.ev0, t.ev1));
-                double span_sum = 0.;
-                for (int i = 0; i < nb; ++i) span_sum += (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
-                for (int i = 0; i < nb; ++i) {
-                    iters_out[t.f0 + i] = t.h_iters[i];
-                    synd_ok_out[t.f0 + i] = t.h_ok[i];
-                    keys_match_out[t.f0 + i] = t.h_km[i];
-                    if (runtime_us_out) {
-                        const double span = (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
-                        runtime_us_out[t.f0 + i] =
-                            span_sum > 0. ? 1e3 * (double)ms * span / span_sum : 1e3 * (double)ms / nb;
-                    }
-                }
-                return QLDPC_OK;
-            };
             auto ensure = [&](TrialSlot &t, int nb) -> int {
                 if (!t.stream) HIP_TRY(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
                 if (!t.ev0) HIP_TRY(hipEventCreate(&t.ev0));
@@ -2540,10 +2609,10 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                 return QLDPC_OK;
             };
             int r = QLDPC_OK;
-            int c = 0;
-            for (int f = lo; f < hi && !r; ++c) {
-                TrialSlot &t = dg->tslot[c & 1];
-                if ((r = harvest(t))) break;
+            for (int f = lo; f < hi && !r;) {
+                TrialSlot &t = dg->tslot[dg->next_slot];
+                dg->next_slot ^= 1;
+                (void)harvest_slot(g, dg, gi, t);  // (a previous chunk, possibly another job's)
                 const int nb = std::min(cap, hi - f);
                 if ((r = ensure(t, nb))) break;
                 auto enqueue = [&]() -> int {
@@ -2571,26 +2640,32 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
                     return QLDPC_OK;
                 };
                 if ((r = enqueue())) {
-                    (void)hipStreamSynchronize(t.stream);  // nothing of this call stays in flight
+                    (void)hipStreamSynchronize(t.stream);  // nothing of this chunk stays in flight
                     break;
                 }
+                t.owner = J;
                 t.f0 = f;
                 t.nb = nb;
                 f += nb;
             }
-            for (auto &t : dg->tslot) {
-                if (r) {  // an error: drain what is in flight, keep the first error
-                    if (t.nb) (void)hipStreamSynchronize(t.stream);
-                    t.nb = 0;
-                } else {
-                    r = harvest(t);
-                }
+            if (r) {  // an error: drain this job's chunks in flight on the device
+                for (auto &t : dg->tslot)
+                    if (t.owner == J) {
+                        (void)hipStreamSynchronize(t.stream);
+                        t.nb = 0;
+                        t.owner = nullptr;
+                    }
             }
             return r;
         };
         const int r = body();
-        rcs[gi] = r;
-        if (r) errs[gi] = g_last_error;
+        if (r) {
+            std::lock_guard<std::mutex> lk(dg->trial_mu);
+            if (J->rcs[gi] == QLDPC_OK) {
+                J->rcs[gi] = r;
+                J->errs[gi] = g_last_error;
+            }
+        }
     };
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
@@ -2602,9 +2677,37 @@ int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_pa
         for (auto &t : th) t.join();
     }
     (void)hipSetDevice(prev);
-    for (int gi = 0; gi < G; ++gi)
-        if (rcs[gi]) return fail(rcs[gi], errs[gi]);
+    *job_out = job.release();
     return QLDPC_OK;
+}
+
+int qldpc_run_trials_wait(qldpc_trials_job *job) {
+    if (!job) return fail(QLDPC_EINVAL, "job is NULL");
+    std::unique_ptr<qldpc_trials_job> own(job);
+    qldpc_graph *g = job->g;
+    int prev = 0;
+    HIP_TRY(hipGetDevice(&prev));
+    for (int gi = 0; gi < (int)g->devs.size(); ++gi) {
+        DeviceGraph *dg = g->devs[gi].get();
+        std::lock_guard<std::mutex> lk(dg->trial_mu);
+        if (hipSetDevice(dg->device) != hipSuccess) continue;
+        for (auto &t : dg->tslot)
+            if (t.owner == job) (void)harvest_slot(g, dg, gi, t);
+    }
+    (void)hipSetDevice(prev);
+    for (int gi = 0; gi < (int)job->rcs.size(); ++gi)
+        if (job->rcs[gi]) return fail(job->rcs[gi], job->errs[gi]);
+    return QLDPC_OK;
+}
+
+int qldpc_run_trials(qldpc_graph *g, const qldpc_rate_plan *plan, const qldpc_params *p, double qber, int32_t count,
+                     const uint64_t *seeds, uint64_t seed_add, uint32_t *iters_out, uint8_t *synd_ok_out,
+                     uint8_t *keys_match_out, double *runtime_us_out, double *accurate_qber_out) {
+    qldpc_trials_job *job = nullptr;
+    const int rc = qldpc_run_trials_submit(g, plan, p, qber, count, seeds, seed_add, iters_out, synd_ok_out,
+                                           keys_match_out, runtime_us_out, accurate_qber_out, &job);
+    if (rc) return rc;
+    return qldpc_run_trials_wait(job);
 }
 
 }  // extern "C"

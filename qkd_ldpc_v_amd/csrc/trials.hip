@@ -4,45 +4,58 @@
 // with seeds[f] + seed_add (the simulation loop's `seeds[n] + curr_sim`,
 // :743), Alice's key from uniform_int_distribution<int>(0, 1) draws
 // (fill_random_bits, src/array_and_matrix_operations.cpp:889-901), Bob's key
-// with exactly floor(n*QBER) errors at the first positions of a std::shuffle'd
-// index vector (inject_errors, :904-933).  Draw consumption follows libstdc++
-// 11 exactly: uniform_int_distribution downscales a 64-bit generator with
-// Lemire's nearly-divisionless method (_S_nd over unsigned __int128), and
-// std::shuffle takes the two-swaps-per-draw path (__gen_two_uniform_ints)
-// because (2^64-1)/n >= n.
+// with exactly k = floor(n*QBER) errors at the first positions of a
+// std::shuffle'd index vector (inject_errors, :904-933), then, for
+// QKD_LDPC_RATE_ADAPT, two uniform_int_distribution<int>(0, 1) draws per
+// punctured position (src/qkd_ldpc_algorithm.cpp:1148-1157).  Draw consumption
+// follows libstdc++ 11 exactly: uniform_int_distribution downscales a 64-bit
+// generator with Lemire's nearly-divisionless method (_S_nd over unsigned
+// __int128), and std::shuffle takes the two-swaps-per-draw path
+// (__gen_two_uniform_ints) because (2^64-1)/n >= n.
 //
-// Draws are sequential per trial, so each LANE runs one trial's generator
-// chain (64 trials per wave, their state in VGPRs, every lane taking the same
-// control flow: the shuffle's loop positions are the same for all trials).
-// inject_errors reads only the first k = floor(n*QBER) positions of the
-// shuffled index vector, and libstdc++'s std::shuffle is the forward
-// Fisher-Yates whose step at position i >= 1 swaps a[i] — still i, untouched
-// by the earlier steps — with some a[j], j <= i.  So positions >= k never need
-// storing: a step at i >= k only writes a[j] = i when j < k, and only the
-// steps at i < k swap inside the k-entry prefix.  Per-trial words (Alice's
-// bits, the flips, the prefix, the punctured draws) live in a global
-// workspace interleaved [word][lane] (a wave's access to one word index is one
-// 256-byte line); a second kernel expands them into the byte keys, one
-// workgroup per trial.  The same draws are consumed in the same order, so the
-// keys are the reference's bit for bit.
+// One trial's draws are one sequential stream of D = n + S + 2 n_punct
+// generator outputs (S = the shuffle's draws: n/2 for even n, (n-1)/2 for odd
+// n).  Xoshiro256's state transition is linear over GF(2), so the state at
+// draw d is J_d · s (J_d = M^d, a 256 x 256 bit matrix): the stream is cut
+// into segments of kSeg draws and every segment starts from J_{j kSeg} · s
+// (a host-built table, one matrix per segment index, shared by every n).  A
+// wave runs one segment of 64 trials (one per lane: the segment's control
+// flow and its matrix loads are wave-uniform), so a batch's generation is
+// (batch / 64) x ceil(D / kSeg) independent waves instead of 64 sequential
+// chains of D draws.
 //
-// Two waves per 64 trials: Alice's n draws and the rest of the chain are two
-// independent stretches of one generator stream, and Xoshiro256's state
-// transition is linear over GF(2), so the state at draw n is J_n · s with the
-// 256 x 256 bit matrix J_n = M^n (built on the host once per n).  One wave
-// draws Alice's bits from s, the other starts at J_n · s and runs the shuffle
-// and the punctured draws: the same draws in the same order, in parallel.
+// What each draw means is fixed by its index alone, except that a shuffle
+// draw may be rejected by _S_nd (probability < range / 2^64 per draw: < 1e-9
+// at n = 100k) and then shifts every later draw.  A lane that meets a
+// rejection flags its trial, and the finish kernel reruns that trial's
+// shuffle and punctured draws sequentially (the reference's order exactly).
+//
+// The shuffle: inject_errors reads only the first k positions of the shuffled
+// index vector, and libstdc++'s std::shuffle is the forward Fisher-Yates whose
+// step at position i >= 1 swaps a[i] — still i, untouched by the earlier
+// steps — with some a[p], p <= i.  So a step at i < k is a swap inside the
+// k-prefix (kept: p goes to pbuf[i]), and a step at i >= k only writes
+// a[p] = i when p < k — the LAST such write wins, i.e. the largest i, which
+// the draw kernel keeps with an atomic max per prefix entry (last[p]).  The
+// finish kernel replays the k - 1 prefix swaps in order in LDS, takes last[p]
+// where set, and flips Bob's key at the k resulting positions.  The same
+// draws are consumed in the same order: the keys are the reference's bit for
+// bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
-#include <utility>
+#include <vector>
 
 namespace qldpc {
 namespace {
+
+constexpr int kSeg = 512;            // draws per segment (one wave runs one segment of 64 trials)
+constexpr uint32_t kPrefixLds = 16384;  // k-prefix entries the finish kernel keeps in LDS (a and p: 128 KiB)
 
 struct Xoshiro256pp {
     uint64_t s0, s1, s2, s3;
@@ -72,7 +85,7 @@ struct Xoshiro256pp {
 };
 
 // libstdc++ uniform_int_distribution::_S_nd<unsigned __int128>: a value in
-// [0, range) from a 64-bit generator.
+// [0, range) from a 64-bit generator (the rejection loop included).
 __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
     uint64_t x = g.next();
     uint64_t lo = x * range;
@@ -88,139 +101,233 @@ __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
     return hi;
 }
 
-// Words of one trial's workspace column: Alice's bits, the flips, the
-// k-prefix and the punctured draws (Alice's, Bob's) as bit words.
-struct TrialWs {
-    int words, k, pwords;
-    __host__ __device__ TrialWs(int n, uint64_t n_err, int n_punct)
-        : words((n + 31) / 32), k((int)n_err), pwords((n_punct + 31) / 32) {}
-    __host__ __device__ size_t per_lane() const { return 2 * (size_t)words + (size_t)k + 2 * (size_t)pwords; }
-    __host__ __device__ size_t abits() const { return 0; }
-    __host__ __device__ size_t flips() const { return (size_t)words; }
-    __host__ __device__ size_t perm() const { return 2 * (size_t)words; }
-    __host__ __device__ size_t palice() const { return 2 * (size_t)words + (size_t)k; }
-    __host__ __device__ size_t pbob() const { return 2 * (size_t)words + (size_t)k + (size_t)pwords; }
+// (x / b1, x % b1) of __gen_two_uniform_ints.  For x < 2^51 the quotient
+// through f64 is exact: x and b1 are exact doubles, and when x / b1 is not an
+// integer it lies at least 1 / b1 below the next integer N + 1, more than
+// half an ulp of N + 1 < 2^52 / b1 (b1 (N + 1) <= x + b1 < 2^52) — so the
+// correctly rounded quotient truncates to floor(x / b1).
+__device__ inline void split_two(uint64_t x, uint64_t b1, uint64_t &p1, uint64_t &p2) {
+    if (x < (1ull << 51)) {
+        p1 = (uint64_t)((double)x / (double)b1);
+    } else {
+        p1 = x / b1;
+    }
+    p2 = x - p1 * b1;
+}
+
+// One trial's draw stream: [0, n) Alice's bits, [n, n + S) the shuffle,
+// [n + S, D) the punctured draws (Alice's, Bob's per position).
+struct TrialStream {
+    uint64_t n, S, D;
+    __host__ __device__ TrialStream(int n_, int n_punct)
+        : n((uint64_t)n_), S((n_ % 2 == 0) ? (uint64_t)n_ / 2 : (uint64_t)(n_ - 1) / 2),
+          D((uint64_t)n_ + S + 2 * (uint64_t)n_punct) {}
 };
 
-// jump: J_n as 256 columns of four words (nullptr: one wave runs the whole
-// chain); the grid then has two waves per 64 trials, Alice's bits in the first
-// half of the blocks, the rest of the chain in the second.
-__global__ void __launch_bounds__(64) trials_lanes_kernel(int n, uint64_t n_err, int batch, const uint64_t *seeds,
-                                                          uint64_t seed_add, uint32_t *ws, int n_punct,
-                                                          const uint64_t *__restrict__ jump) {
+// Generator workspace, uint32 words, BP = batch rounded up to 64:
+// pbuf [k][BP] (prefix swap partner of position i < k), last [BP][k] (largest
+// i >= k that wrote prefix entry p; 0 = none), abuf [BP][k] (the prefix when
+// it exceeds LDS), flag [BP] (a rejected shuffle draw: rerun serially).
+struct TrialWs {
+    size_t k, BP;
+    __host__ __device__ TrialWs(uint64_t k_, int batch) : k((size_t)k_), BP(((size_t)batch + 63) / 64 * 64) {}
+    __host__ __device__ size_t pbuf() const { return 0; }
+    __host__ __device__ size_t last() const { return k * BP; }
+    __host__ __device__ size_t abuf() const { return 2 * k * BP; }
+    __host__ __device__ size_t flag() const { return 3 * k * BP; }
+    __host__ __device__ size_t words() const { return 3 * k * BP + BP; }
+};
+
+// Draw kernel: block (segment j, trial group of 64), one lane per trial.
+__global__ void __launch_bounds__(64) trials_draw_kernel(int n, uint32_t k, int n_punct, int batch,
+                                                         const uint64_t *__restrict__ seeds, uint64_t seed_add,
+                                                         const uint64_t *__restrict__ jt, int wide,
+                                                         uint8_t *__restrict__ alice, uint8_t *__restrict__ bob,
+                                                         uint8_t *__restrict__ palice, uint8_t *__restrict__ pbob,
+                                                         uint32_t *__restrict__ ws) {
     const int lane = threadIdx.x;
-    const int nblk = (batch + 63) / 64;
-    const bool split = jump != nullptr;
-    const bool tail = split && (int)blockIdx.x >= nblk;  // this wave starts at draw n
-    const int blk = tail ? (int)blockIdx.x - nblk : (int)blockIdx.x;
-    const int f = blk * 64 + lane;
-    const TrialWs L(n, n_err, n_punct);
-    // this wave's 64 columns, [word][lane]
-    uint32_t *col = ws + (size_t)blk * L.per_lane() * 64 + lane;
-    auto at = [&](size_t word) -> uint32_t & { return col[word * 64]; };
-    Xoshiro256pp g((f < batch ? seeds[f] : 0ull) + seed_add);
-    if (!tail) {
-        // fill_random_bits: uniform_int_distribution<int>(0, 1) -> _S_nd(g, 2),
-        // which never rejects: the top bit of each draw.
-        for (int w = 0; w < L.words; ++w) {
-            uint32_t v = 0;
-            const int nb = (n - 32 * w < 32) ? n - 32 * w : 32;
-            for (int b = 0; b < nb; ++b) v |= (uint32_t)(g.next() >> 63) << b;
-            at(L.abits() + w) = v;
-        }
-        if (split) return;
-    } else {
-        // the state after Alice's n draws: J_n · s over GF(2) (columns by
-        // wave-uniform loads)
-        const uint64_t s[4] = {g.s0, g.s1, g.s2, g.s3};
-        uint64_t r[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 256; ++j) {
-            const uint64_t m = 0ull - ((s[j >> 6] >> (j & 63)) & 1ull);
+    const int f = (int)blockIdx.y * 64 + lane;
+    const bool act = f < batch;
+    const TrialStream T(n, n_punct);
+    const TrialWs W(k, batch);
+    const uint64_t seg = blockIdx.x;
+    uint64_t d = seg * kSeg;
+    const uint64_t d1 = (d + kSeg < T.D) ? d + kSeg : T.D;
+    Xoshiro256pp g((act ? seeds[f] : 0ull) + seed_add);
+    if (seg > 0) {  // the state at draw seg * kSeg: J · s over GF(2), columns by wave-uniform loads
+        const uint64_t *J = jt + seg * 1024;
+        const uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
+        uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] ^= jump[4 * j + q] & m;
-        }
-        g.s0 = r[0];
-        g.s1 = r[1];
-        g.s2 = r[2];
-        g.s3 = r[3];
-    }
-    for (int w = 0; w < L.words; ++w) at(L.flips() + w) = 0u;
-    const uint32_t k = (uint32_t)n_err;
-    if (k > 0) {
-        for (uint32_t e = 0; e < k; ++e) at(L.perm() + e) = e;
-        // one swap of std::shuffle, a[pos] <-> a[p] (p <= pos), on the k-prefix
-        auto swap_at = [&](uint32_t pos, uint32_t p) {
-            if (pos < k) {  // (pos is the same on every lane)
-                const uint32_t t = at(L.perm() + pos), u = at(L.perm() + p);
-                at(L.perm() + pos) = u;
-                at(L.perm() + p) = t;
-            } else if (p < k) {
-                at(L.perm() + p) = pos;  // a[pos] == pos until its own step
+        for (int w = 0; w < 4; ++w) {
+            const uint64_t sw = st[w];
+#pragma unroll 8
+            for (int b = 0; b < 64; ++b) {
+                const uint64_t m = 0ull - ((sw >> b) & 1ull);
+                const uint64_t *c = J + 4 * (64 * w + b);
+                r0 ^= c[0] & m;
+                r1 ^= c[1] & m;
+                r2 ^= c[2] & m;
+                r3 ^= c[3] & m;
             }
-        };
-        // std::shuffle(first, last, g), libstdc++ 11 (bits/stl_algo.h)
-        uint64_t i = 1;
-        if ((n & 1) == 0) {
-            swap_at(1, (uint32_t)draw_below(g, 2));
-            i = 2;
         }
-        while (i != (uint64_t)n) {
-            const uint64_t b0 = i + 1, b1 = i + 2;  // __gen_two_uniform_ints(b0, b0 + 1)
-            const uint64_t x = draw_below(g, b0 * b1);
-            uint64_t p1, p2;
-            if (x < 0x100000000ull) {  // 32-bit divide when it fits (n <= 65535 always)
-                const uint32_t x32 = (uint32_t)x, d32 = (uint32_t)b1;
-                p1 = x32 / d32;
-                p2 = x32 - (uint32_t)p1 * d32;
-            } else {
-                p1 = x / b1;
-                p2 = x % b1;
+        g.s0 = r0;
+        g.s1 = r1;
+        g.s2 = r2;
+        g.s3 = r3;
+    }
+    // fill_random_bits: _S_nd(g, 2) never rejects — the top bit of each draw.
+    // Bob's key starts as a copy of Alice's; the finish kernel flips it.
+    const uint64_t ae = d1 < T.n ? d1 : T.n;
+    if (d < ae) {
+        uint8_t *ap = alice + (size_t)f * (size_t)n;
+        uint8_t *bp = bob + (size_t)f * (size_t)n;
+        if (wide) {  // n % 16 == 0 and 16-byte aligned keys: one 16-byte store per 16 draws
+            for (; d < ae; d += 16) {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) v |= (uint32_t)(g.next() >> 63) << (8 * b);
+                    w[q] = v;
+                }
+                if (act) {
+                    const uint4 v4 = make_uint4(w[0], w[1], w[2], w[3]);
+                    *reinterpret_cast<uint4 *>(ap + d) = v4;
+                    *reinterpret_cast<uint4 *>(bp + d) = v4;
+                }
             }
-            swap_at((uint32_t)i, (uint32_t)p1);
-            swap_at((uint32_t)i + 1, (uint32_t)p2);
-            i += 2;
-        }
-        for (uint32_t e = 0; e < k; ++e) {  // inject_errors: flip pos[0 .. k)
-            const uint32_t p = at(L.perm() + e);
-            at(L.flips() + (p >> 5)) |= 1u << (p & 31);
+        } else {
+            for (; d < ae; ++d) {
+                const uint8_t v = (uint8_t)(g.next() >> 63);
+                if (act) {
+                    ap[d] = v;
+                    bp[d] = v;
+                }
+            }
         }
     }
-    // QKD_LDPC_RATE_ADAPT continues the trial's generator: two
-    // uniform_int_distribution<int>(0, 1) draws (Alice, then Bob) per
-    // punctured position, in ascending position order
-    // (src/qkd_ldpc_algorithm.cpp:1148-1157).
-    for (int w = 0; w < L.pwords; ++w) {
-        uint32_t va = 0, vb = 0;
-        const int nb = (n_punct - 32 * w < 32) ? n_punct - 32 * w : 32;
-        for (int b = 0; b < nb; ++b) {
-            va |= (uint32_t)(g.next() >> 63) << b;
-            vb |= (uint32_t)(g.next() >> 63) << b;
+    // std::shuffle (libstdc++ 11, bits/stl_algo.h), one step per position
+    uint32_t *pbuf = ws + W.pbuf();
+    uint32_t *last = ws + W.last() + (size_t)f * W.k;
+    auto record = [&](uint64_t pos, uint64_t p) {
+        if (pos < k) {  // a swap inside the prefix (pos is wave-uniform): replayed in order later
+            if (act) pbuf[pos * W.BP + f] = (uint32_t)p;
+        } else if (p < k && act) {  // a[p] = pos; the largest pos wins
+            atomicMax(last + p, (uint32_t)pos);
         }
-        at(L.palice() + w) = va;
-        at(L.pbob() + w) = vb;
+    };
+    const uint64_t se = d1 < T.n + T.S ? d1 : T.n + T.S;
+    bool rejected = false;
+    for (; d < se; ++d) {
+        const uint64_t t = d - T.n;
+        if ((n & 1) == 0 && t == 0) {  // even n: the first swap takes a single (0, 1) draw
+            record(1, g.next() >> 63);
+            continue;
+        }
+        const uint64_t i = (n & 1) == 0 ? 2 * t : 2 * t + 1;
+        const uint64_t b1 = i + 2, range = (i + 1) * b1;  // __gen_two_uniform_ints(i + 1, i + 2)
+        const uint64_t x = g.next();
+        const uint64_t lo = x * range;
+        if (lo < range) {
+            const uint64_t threshold = (0 - range) % range;
+            if (lo < threshold) rejected = true;  // every later draw of this trial shifts
+        }
+        uint64_t p1, p2;
+        split_two(__umul64hi(x, range), b1, p1, p2);
+        record(i, p1);
+        record(i + 1, p2);
+    }
+    if (rejected && act) ws[W.flag() + f] = 1u;
+    // QKD_LDPC_RATE_ADAPT continues the trial's generator: Alice's then Bob's
+    // draw per punctured position, in ascending position order.
+    for (; d < d1; ++d) {
+        const uint64_t t = d - T.n - T.S;
+        const uint8_t v = (uint8_t)(g.next() >> 63);
+        if (act) ((t & 1) ? pbob : palice)[(size_t)f * (size_t)n_punct + (t >> 1)] = v;
     }
 }
 
-// The keys as bytes, one workgroup per trial: Alice's, Bob's (Alice's xor the
-// flips) and the punctured draws.
-__global__ void __launch_bounds__(256) trials_expand_kernel(int n, uint64_t n_err, int batch, const uint32_t *ws,
-                                                            uint8_t *alice, uint8_t *bob, int n_punct,
-                                                            uint8_t *punct_alice, uint8_t *punct_bob) {
+// Finish kernel, one workgroup per trial: replay the prefix swaps, merge the
+// last writers, flip Bob's key at the k chosen positions.  A trial with a
+// rejected shuffle draw (or every trial under force_serial) reruns its
+// shuffle and punctured draws sequentially from the state after Alice's bits.
+__global__ void __launch_bounds__(256) trials_finish_kernel(int n, uint32_t k, int n_punct, int batch,
+                                                            const uint64_t *__restrict__ seeds, uint64_t seed_add,
+                                                            const uint8_t *__restrict__ alice,
+                                                            uint8_t *__restrict__ bob, uint8_t *__restrict__ palice,
+                                                            uint8_t *__restrict__ pbob, uint32_t *__restrict__ ws,
+                                                            int force_serial) {
+    extern __shared__ uint32_t sh[];
     const int f = blockIdx.x;
-    const TrialWs L(n, n_err, n_punct);
-    const uint32_t *col = ws + (size_t)(f / 64) * L.per_lane() * 64 + (f % 64);
-    auto at = [&](size_t word) { return col[word * 64]; };
-    uint8_t *a = alice + (size_t)f * n;
-    uint8_t *b = bob + (size_t)f * n;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t av = (at(L.abits() + (i >> 5)) >> (i & 31)) & 1u;
-        const uint32_t fv = (at(L.flips() + (i >> 5)) >> (i & 31)) & 1u;
-        a[i] = (uint8_t)av;
-        b[i] = (uint8_t)(av ^ fv);
+    const TrialWs W(k, batch);
+    const bool in_lds = k <= kPrefixLds;
+    uint32_t *a = in_lds ? sh : ws + W.abuf() + (size_t)f * W.k;
+    uint32_t *pl = in_lds ? sh + k : nullptr;  // this trial's pbuf column, staged
+    const bool serial = force_serial || ws[W.flag() + f] != 0u;
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        a[j] = j;
+        if (pl && !serial) pl[j] = j ? ws[W.pbuf() + (size_t)j * W.BP + f] : 0u;
     }
-    for (int j = threadIdx.x; j < n_punct; j += blockDim.x) {
-        punct_alice[(size_t)f * n_punct + j] = (uint8_t)((at(L.palice() + (j >> 5)) >> (j & 31)) & 1u);
-        punct_bob[(size_t)f * n_punct + j] = (uint8_t)((at(L.pbob() + (j >> 5)) >> (j & 31)) & 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!serial) {
+            if (pl) {
+                for (uint32_t pos = 1; pos < k; ++pos) {  // a[pos] == pos until its own step
+                    const uint32_t p = pl[pos];
+                    const uint32_t t = a[p];
+                    a[p] = pos;
+                    a[pos] = t;
+                }
+            } else {
+                for (uint32_t pos = 1; pos < k; ++pos) {
+                    const uint32_t p = ws[W.pbuf() + (size_t)pos * W.BP + f];
+                    const uint32_t t = a[p];
+                    a[p] = pos;
+                    a[pos] = t;
+                }
+            }
+        } else {
+            Xoshiro256pp g(seeds[f] + seed_add);
+            for (int i = 0; i < n; ++i) (void)g.next();  // Alice's draws (already written)
+            auto swap_at = [&](uint64_t pos, uint64_t p) {
+                if (pos < k) {
+                    const uint32_t t = a[pos], u = a[p];
+                    a[pos] = u;
+                    a[p] = t;
+                } else if (p < k) {
+                    a[p] = (uint32_t)pos;
+                }
+            };
+            uint64_t i = 1;
+            if ((n & 1) == 0) {
+                swap_at(1, draw_below(g, 2));
+                i = 2;
+            }
+            while (i != (uint64_t)n) {
+                const uint64_t b1 = i + 2;
+                uint64_t p1, p2;
+                split_two(draw_below(g, (i + 1) * b1), b1, p1, p2);
+                swap_at(i, p1);
+                swap_at(i + 1, p2);
+                i += 2;
+            }
+            for (int q = 0; q < n_punct; ++q) {
+                palice[(size_t)f * n_punct + q] = (uint8_t)(g.next() >> 63);
+                pbob[(size_t)f * n_punct + q] = (uint8_t)(g.next() >> 63);
+            }
+        }
+    }
+    __syncthreads();
+    // inject_errors: flip Bob's key at a[0 .. k)
+    const uint32_t *last = ws + W.last() + (size_t)f * W.k;
+    const uint8_t *ap = alice + (size_t)f * (size_t)n;
+    uint8_t *bp = bob + (size_t)f * (size_t)n;
+    for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
+        const uint32_t lw = serial ? 0u : last[j];
+        const uint32_t pos = lw ? lw : a[j];
+        bp[pos] = (uint8_t)(ap[pos] ^ 1u);
     }
 }
 
@@ -344,30 +451,6 @@ void xo_jump_matrix(uint64_t d, uint64_t *J) {
         }
     }
 }
-// J_n on a device, built and uploaded once per (device, n) for the process.
-std::mutex g_jump_mu;
-std::map<std::pair<int, int>, uint64_t *> g_jump;
-hipError_t jump_on_device(int n, const uint64_t **out) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> lk(g_jump_mu);
-    auto it = g_jump.find({dev, n});
-    if (it == g_jump.end()) {
-        uint64_t J[1024];
-        xo_jump_matrix((uint64_t)n, J);
-        uint64_t *d = nullptr;
-        if ((e = hipMalloc(&d, sizeof J)) != hipSuccess) return e;
-        if ((e = hipMemcpy(d, J, sizeof J, hipMemcpyHostToDevice)) != hipSuccess) {
-            (void)hipFree(d);
-            return e;
-        }
-        it = g_jump.emplace(std::make_pair(dev, n), d).first;
-    }
-    *out = it->second;
-    return hipSuccess;
-}
-
 }  // namespace
 
 int xoshiro_jump_check(uint64_t seed, uint64_t d, uint64_t *state_out) {
@@ -386,29 +469,118 @@ int xoshiro_jump_check(uint64_t seed, uint64_t d, uint64_t *state_out) {
     return 0;
 }
 
+namespace {
+
+// Jump tables: entry j = J_{j kSeg} (column-major, 1024 words), entry 0 the
+// identity, entry j + 1 = J_kSeg · entry j by four-Russians tables of J_kSeg
+// (32 byte-groups x 256 column combinations).  One table per device, shared by
+// every n; it grows to the longest stream asked for and is never freed (a
+// retired shorter copy may still be read by a launch in flight).
+struct JumpTable {
+    std::vector<uint64_t> host;  // entries x 1024 words
+    uint64_t *dev = nullptr;
+    size_t dev_entries = 0;
+};
+std::mutex g_jt_mu;
+std::map<int, JumpTable> g_jt;
+std::vector<uint64_t> g_jt_host;  // host entries, shared by the devices
+std::vector<uint64_t> g_jl_russ;  // J_kSeg as 32 x 256 column combinations (4 words each)
+
+void jt_extend_host(size_t entries) {  // (g_jt_mu held)
+    if (g_jt_host.empty()) {
+        uint64_t I[1024];
+        xo_jump_matrix(0, I);
+        g_jt_host.assign(I, I + 1024);
+        uint64_t J[1024];
+        xo_jump_matrix((uint64_t)kSeg, J);
+        g_jl_russ.assign(32 * 256 * 4, 0);
+        for (int grp = 0; grp < 32; ++grp)
+            for (int b = 1; b < 256; ++b) {
+                const int low = __builtin_ctz((unsigned)b);
+                const uint64_t *prev = &g_jl_russ[((size_t)grp * 256 + (b & (b - 1))) * 4];
+                const uint64_t *col = J + 4 * (8 * grp + low);
+                uint64_t *dst = &g_jl_russ[((size_t)grp * 256 + b) * 4];
+                for (int q = 0; q < 4; ++q) dst[q] = prev[q] ^ col[q];
+            }
+    }
+    while (g_jt_host.size() / 1024 < entries) {
+        const uint64_t *B = &g_jt_host[g_jt_host.size() - 1024];
+        uint64_t C[1024];
+        for (int c = 0; c < 256; ++c) {  // column c of J_kSeg · B
+            uint64_t r[4] = {0, 0, 0, 0};
+            for (int grp = 0; grp < 32; ++grp) {
+                const unsigned byte = (unsigned)(B[4 * c + grp / 8] >> (8 * (grp % 8))) & 0xffu;
+                const uint64_t *t = &g_jl_russ[((size_t)grp * 256 + byte) * 4];
+                for (int q = 0; q < 4; ++q) r[q] ^= t[q];
+            }
+            std::memcpy(C + 4 * c, r, sizeof r);
+        }
+        g_jt_host.insert(g_jt_host.end(), C, C + 1024);
+    }
+}
+
+hipError_t jump_table_on_device(size_t entries, const uint64_t **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_jt_mu);
+    JumpTable &t = g_jt[dev];
+    if (t.dev_entries < entries) {
+        const size_t want = std::max(entries, 2 * t.dev_entries);
+        jt_extend_host(want);
+        uint64_t *d = nullptr;
+        if ((e = hipMalloc(&d, want * 1024 * sizeof(uint64_t))) != hipSuccess) return e;
+        if ((e = hipMemcpy(d, g_jt_host.data(), want * 1024 * sizeof(uint64_t), hipMemcpyHostToDevice)) !=
+            hipSuccess) {
+            (void)hipFree(d);
+            return e;
+        }
+        t.dev = d;  // (the previous, shorter table is left allocated: a launch may still read it)
+        t.dev_entries = want;
+    }
+    *out = t.dev;
+    return hipSuccess;
+}
+
+}  // namespace
+
 size_t trials_scratch_words(int n, uint64_t n_err, int n_punct, int batch) {
-    return TrialWs(n, n_err, n_punct).per_lane() * 64 * (size_t)((batch + 63) / 64);
+    (void)n;
+    (void)n_punct;
+    return TrialWs(n_err, batch).words();
 }
 
 hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds, uint64_t seed_add, uint8_t *alice,
                          uint8_t *bob, uint32_t *scratch, int n_punct, uint8_t *punct_alice, uint8_t *punct_bob,
                          hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    if (!scratch) return hipErrorInvalidValue;
-    // two waves per 64 trials (QLDPC_TRIAL_SPLIT=0: one, A/B)
-    const uint64_t *jump = nullptr;
-    const char *env = std::getenv("QLDPC_TRIAL_SPLIT");
-    if (!(env && std::strcmp(env, "0") == 0)) {
-        hipError_t je = jump_on_device(n, &jump);
-        if (je != hipSuccess) return je;
-    }
-    const int nblk = (batch + 63) / 64;
-    hipLaunchKernelGGL(trials_lanes_kernel, dim3(jump ? 2 * nblk : nblk), dim3(64), 0, stream, n, n_err, batch,
-                       seeds, seed_add, scratch, n_punct, jump);
-    hipError_t e = hipGetLastError();
+    if (!scratch || n <= 0 || n_err == 0 || n_err > (uint64_t)n || n_punct < 0) return hipErrorInvalidValue;
+    const TrialStream T(n, n_punct);
+    const TrialWs W(n_err, batch);
+    const size_t nseg = (size_t)((T.D + kSeg - 1) / kSeg);
+    const int ngrp = (batch + 63) / 64;
+    if (nseg > 0x7fffffff || ngrp > 65535) return hipErrorInvalidValue;
+    const uint64_t *jt = nullptr;
+    hipError_t e = jump_table_on_device(nseg, &jt);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(trials_expand_kernel, dim3(batch), dim3(256), 0, stream, n, n_err, batch, scratch, alice, bob,
-                       n_punct, punct_alice, punct_bob);
+    // last[] (0 = no writer) and the rejection flags start cleared
+    if ((e = hipMemsetAsync(scratch + W.last(), 0, W.k * W.BP * sizeof(uint32_t), stream)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(scratch + W.flag(), 0, W.BP * sizeof(uint32_t), stream)) != hipSuccess) return e;
+    const int wide = (n % 16 == 0) && ((reinterpret_cast<uintptr_t>(alice) | reinterpret_cast<uintptr_t>(bob)) & 15) == 0;
+    hipLaunchKernelGGL(trials_draw_kernel, dim3((unsigned)nseg, (unsigned)ngrp), dim3(64), 0, stream, n,
+                       (uint32_t)n_err, n_punct, batch, seeds, seed_add, jt, wide, alice, bob, punct_alice, punct_bob,
+                       scratch);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // QLDPC_TRIAL_SERIAL=1: every trial takes the sequential rerun (the path a
+    // rejected draw takes), for the parity tests
+    const char *env = std::getenv("QLDPC_TRIAL_SERIAL");
+    const int force_serial = env && std::strcmp(env, "1") == 0;
+    const size_t lds = n_err <= kPrefixLds ? 2 * (size_t)n_err * sizeof(uint32_t) : 0;
+    if (lds > 65536 && (e = hipFuncSetAttribute(reinterpret_cast<const void *>(trials_finish_kernel),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(trials_finish_kernel, dim3(batch), dim3(256), lds, stream, n, (uint32_t)n_err, n_punct, batch,
+                       seeds, seed_add, alice, bob, punct_alice, punct_bob, scratch, force_serial);
     return hipGetLastError();
 }
 

@@ -100,6 +100,34 @@ class TrialsOutput:
     accurate_qber: float    # trial_result.accurate_QBER (the same for every trial)
 
 
+class TrialsJob:
+    """One combination's trials in flight (qldpc_run_trials_submit); keeps the
+    graph, the rate plan and the output arrays alive until wait()."""
+
+    def __init__(self, graph, plan, count: int):
+        self.graph, self.plan, self.handle = graph, plan, None
+        self.it = np.empty(count, np.uint32)
+        self.ok = np.empty(count, np.uint8)
+        self.km = np.empty(count, np.uint8)
+        self.rt = np.empty(count, np.float64)
+        self.q = ctypes.c_double(0.0)
+        self._out = None
+
+    def wait(self) -> TrialsOutput:
+        if self._out is None:
+            h, self.handle = self.handle, None
+            check(lib().qldpc_run_trials_wait(h), "qldpc_run_trials_wait")
+            self._out = TrialsOutput(self.it, self.ok, self.km, self.rt, self.q.value)
+        return self._out
+
+    def __del__(self):
+        if self.handle is not None:  # a job is always completed (its slots hold our arrays)
+            try:
+                lib().qldpc_run_trials_wait(self.handle)
+            except Exception:
+                pass
+
+
 def _canonical_adjacency(H: HMatrix) -> bool:
     """check_nodes rows ascending and bit_nodes their ascending transpose: the
     reference's slot pairing is then the edge itself (src/qkd_ldpc_algorithm.cpp:
@@ -274,6 +302,25 @@ class Graph:
                                      ok.ctypes.data, km.ctypes.data, rt.ctypes.data, ctypes.byref(q)),
               "qldpc_run_trials")
         return TrialsOutput(it, ok, km, rt, q.value)
+
+    def submit_trials(self, params: Params, qber: float, seeds, seed_add: int = 0,
+                      plan: "RatePlan | None" = None) -> "TrialsJob":
+        """run_trials in two halves (qldpc_run_trials_submit / _wait): the trials
+        are on the devices when this returns; TrialsJob.wait() -> TrialsOutput.
+        Lets a driver put the next combination on the GPUs before it collects
+        this one."""
+        sd = np.ascontiguousarray(seeds, np.uint64)
+        cnt = int(sd.size)
+        job = TrialsJob(self, plan, cnt)
+        p = params.c()
+        h = ctypes.c_void_p()
+        check(lib().qldpc_run_trials_submit(self._g, None if plan is None else plan.handle, ctypes.byref(p),
+                                            float(qber), cnt, sd.ctypes.data, int(seed_add) & 0xFFFFFFFFFFFFFFFF,
+                                            job.it.ctypes.data, job.ok.ctypes.data, job.km.ctypes.data,
+                                            job.rt.ctypes.data, ctypes.byref(job.q), ctypes.byref(h)),
+              "qldpc_run_trials_submit")
+        job.handle = h
+        return job
 
     def rate_plan(self, punctured, shortened) -> "RatePlan":
         return RatePlan(self, punctured, shortened)

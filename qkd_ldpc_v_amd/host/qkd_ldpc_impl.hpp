@@ -549,40 +549,84 @@ struct BatchTrial {
     double runtime_us;  // trial_result::runtime (qldpc_run_trials: share of the chunk window)
 };
 
+// One combination's trials on the devices (qldpc_run_trials_submit): holds
+// the device graph, the rate plan and the result arrays until wait() (which
+// the destructor also does, so a job never leaves chunks behind).
+class TrialsJob {
+  public:
+    TrialsJob(std::shared_ptr<GraphEntry> e, qldpc_rate_plan *plan, size_t count)
+        : e_(std::move(e)), plan_(plan, qldpc_rate_plan_destroy), it_(count), ok_(count), km_(count), rt_(count) {}
+    TrialsJob(const TrialsJob &) = delete;
+    TrialsJob &operator=(const TrialsJob &) = delete;
+    ~TrialsJob() {
+        if (h_) (void)qldpc_run_trials_wait(h_);
+    }
+    // Per trial {iterations_num, syndromes_match, keys_match, runtime_us}.
+    std::vector<BatchTrial> wait() {
+        qldpc_trials_job *h = h_;
+        h_ = nullptr;
+        if (h && qldpc_run_trials_wait(h)) throw std::runtime_error(qldpc_last_error());
+        std::vector<BatchTrial> out(it_.size());
+        for (size_t t = 0; t < out.size(); ++t) out[t] = {it_[t], ok_[t] != 0, km_[t] != 0, rt_[t]};
+        return out;
+    }
+    double accurate_qber() const { return q_; }
+
+  private:
+    template <class Matrix>
+    friend std::unique_ptr<TrialsJob> submit_trials(const Matrix &, double, const std::vector<size_t> &, size_t,
+                                                    double, double, const DecodeConfig &, const std::vector<int> *,
+                                                    const std::vector<int> *);
+    std::shared_ptr<GraphEntry> e_;
+    std::unique_ptr<qldpc_rate_plan, void (*)(qldpc_rate_plan *)> plan_;
+    std::vector<uint32_t> it_;
+    std::vector<uint8_t> ok_, km_;
+    std::vector<double> rt_;
+    double q_ = 0.;
+    qldpc_trials_job *h_ = nullptr;
+};
+
 // The batch seam of the simulation loop: run_trial for every seed of one
 // combination (QKD_LDPC_batch_simulation's pool.detach_loop over run_trial,
-// src/simulation.cpp:721-746) as one qldpc_run_trials call — trial t uses
-// the seed seeds[t] + seed_add (the loop's `seeds[n] + curr_sim`, :743);
-// the trials are generated, decoded and compared on the drop-in's devices,
-// sharded over them.  punctured / shortened (ascending, both or neither):
-// CFG.ENABLE_CODE_RATE_ADAPTATION's QKD_LDPC_RATE_ADAPT, else QKD_LDPC.
-// accurate_qber (nullable): every trial's trial_result::accurate_QBER.
+// src/simulation.cpp:721-746), submitted as one qldpc_run_trials_submit —
+// trial t uses the seed seeds[t] + seed_add (the loop's `seeds[n] +
+// curr_sim`, :743); the trials are generated, decoded and compared on the
+// drop-in's devices, sharded over them, while the caller goes on (e.g. to
+// submit the next combination).  punctured / shortened (ascending, both or
+// neither): CFG.ENABLE_CODE_RATE_ADAPTATION's QKD_LDPC_RATE_ADAPT, else
+// QKD_LDPC.  Throws run_trial's errors (e.g. "Key size ... is too small for
+// QBER.").
 template <class Matrix>
-std::vector<BatchTrial> run_trials(const Matrix &H, double qber, const std::vector<size_t> &seeds, size_t seed_add,
-                                   double primary, double secondary, const DecodeConfig &cfg,
-                                   const std::vector<int> *punctured, const std::vector<int> *shortened,
-                                   double *accurate_qber) {
+std::unique_ptr<TrialsJob> submit_trials(const Matrix &H, double qber, const std::vector<size_t> &seeds,
+                                         size_t seed_add, double primary, double secondary, const DecodeConfig &cfg,
+                                         const std::vector<int> *punctured, const std::vector<int> *shortened) {
     auto e = graph_cache().get(H);
     qldpc_rate_plan *plan = nullptr;
     if (punctured && shortened &&
         qldpc_rate_plan_create(e->g.get(), (int32_t)punctured->size(), punctured->data(), (int32_t)shortened->size(),
                                shortened->data(), &plan))
         raise("qldpc_rate_plan_create");
-    std::unique_ptr<qldpc_rate_plan, void (*)(qldpc_rate_plan *)> plan_guard(plan, qldpc_rate_plan_destroy);
-    const size_t count = seeds.size();
+    std::unique_ptr<TrialsJob> job(new TrialsJob(e, plan, seeds.size()));
     std::vector<uint64_t> sd(seeds.begin(), seeds.end());
-    std::vector<uint32_t> it(count);
-    std::vector<uint8_t> ok(count), km(count);
-    std::vector<double> rt(count);
-    double q = 0.;
     const qldpc_params p{cfg.algorithm, (int32_t)cfg.max_iterations, cfg.thr_enabled ? 1 : 0, 0, cfg.thr, primary,
                          secondary};
-    if (qldpc_run_trials(e->g.get(), plan, &p, qber, (int32_t)count, sd.data(), (uint64_t)seed_add, it.data(),
-                         ok.data(), km.data(), rt.data(), &q))
-        throw std::runtime_error(qldpc_last_error());  // e.g. run_trial's "Key size ... is too small for QBER."
-    if (accurate_qber) *accurate_qber = q;
-    std::vector<BatchTrial> out(count);
-    for (size_t t = 0; t < count; ++t) out[t] = {it[t], ok[t] != 0, km[t] != 0, rt[t]};
+    if (qldpc_run_trials_submit(e->g.get(), plan, &p, qber, (int32_t)sd.size(), sd.data(), (uint64_t)seed_add,
+                                job->it_.data(), job->ok_.data(), job->km_.data(), job->rt_.data(), &job->q_,
+                                &job->h_))
+        throw std::runtime_error(qldpc_last_error());
+    return job;
+}
+
+// run_trials: one combination, submitted and collected (accurate_qber
+// nullable: every trial's trial_result::accurate_QBER).
+template <class Matrix>
+std::vector<BatchTrial> run_trials(const Matrix &H, double qber, const std::vector<size_t> &seeds, size_t seed_add,
+                                   double primary, double secondary, const DecodeConfig &cfg,
+                                   const std::vector<int> *punctured, const std::vector<int> *shortened,
+                                   double *accurate_qber) {
+    auto job = submit_trials(H, qber, seeds, seed_add, primary, secondary, cfg, punctured, shortened);
+    auto out = job->wait();
+    if (accurate_qber) *accurate_qber = job->accurate_qber();
     return out;
 }
 

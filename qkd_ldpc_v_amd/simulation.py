@@ -404,10 +404,19 @@ def prepare(cfg: Config, matrix_paths: list[str]):
 # ---- trials on the GPU + statistics -------------------------------------------
 def shard_ranges(total: int, shards: int) -> list[tuple[int, int]]:
     """Contiguous trial slices [b, e) of ceil(total / shards) trials, one per
-    shard; trailing shards may be short or empty."""
+    shard; trailing shards may be short or empty — the
+    slices qldpc_run_trials gives the graph's devices (qldpc_shard_range)."""
+    import ctypes
+
+    from ._lib import check, lib
+
     shards = max(1, int(shards))
-    per = -(-total // shards)
-    return [(min(total, k * per), min(total, (k + 1) * per)) for k in range(shards)]
+    out = []
+    for k in range(shards):
+        lo, hi = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().qldpc_shard_range(int(total), shards, k, ctypes.byref(lo), ctypes.byref(hi)), "qldpc_shard_range")
+        out.append((lo.value, hi.value))
+    return out
 
 
 def run(cfg: Config, mats, combos, device: int = 0, log=print, devices=None):
@@ -427,7 +436,9 @@ def run(cfg: Config, mats, combos, device: int = 0, log=print, devices=None):
     seeds = trial_seeds(cfg.simulation_seed, cfg.trials_number)
     graphs = {}  # matrix -> Graph replicated on devs
     results = []
-    for sim, c in enumerate(combos):
+
+    def submit(sim):
+        c = combos[sim]
         path, H = mats[c.matrix_index]
         p = Params(cfg.decoding_algorithm, cfg.max_iterations, cfg.threshold_enabled, cfg.threshold, c.primary,
                    c.secondary)
@@ -436,7 +447,23 @@ def run(cfg: Config, mats, combos, device: int = 0, log=print, devices=None):
         g = graphs[c.matrix_index]
         plan = g.rate_plan(c.punctured, c.shortened) if c.punctured is not None else None
         # trial seed = seeds[n] + curr_sim (:743)
-        out = g.run_trials(p, c.config_qber, seeds, seed_add=sim, plan=plan)
+        return g.submit_trials(p, c.config_qber, seeds, seed_add=sim, plan=plan)
+
+    def try_submit(sim):  # an error (run_trial's "too small for QBER") is raised at its own turn
+        try:
+            return submit(sim)
+        except Exception as e:  # noqa: BLE001
+            return e
+
+    # combination sim + 1 goes onto the GPUs before combination sim is
+    # collected, so its generation overlaps the tail of sim's decode
+    nxt = try_submit(0) if combos else None
+    for sim, c in enumerate(combos):
+        job, nxt = nxt, (try_submit(sim + 1) if sim + 1 < len(combos) else None)
+        if isinstance(job, Exception):
+            raise job
+        out = job.wait()
+        path, H = mats[c.matrix_index]
         r = _stats(cfg, sim, os.path.basename(path), H, c, out.accurate_qber, out.iterations.astype(np.int64),
                    out.synd_ok.astype(bool), out.keys_match.astype(bool), out.runtime_us)
         results.append(r)
@@ -451,8 +478,11 @@ def throughput_stats(out_len: int, runtime_us: np.ndarray, trials_number: int, r
     the RTT when CONSIDER_RTT), mean and population std over TRIALS_NUMBER, each
     truncated to an integer as the reference's size_t fields.  runtime_us: the
     trial_result::runtime of each trial (qldpc_run_trials: its share of its
-    chunk's measured window by its own decode span)."""
-    rt = np.asarray(runtime_us, np.float64)
+    chunk's measured window by its own decode span), held — as the reference's
+    std::chrono::microseconds field holds it, and as the C++ batch seam
+    (simulation_batch.cpp) stores it — in whole microseconds, rounded to
+    nearest and at least 1."""
+    rt = np.maximum(1.0, np.floor(np.asarray(runtime_us, np.float64) + 0.5))
     denom = rt + (rtt_ms * 1000.0 if rtt_ms is not None else 0.0)
     tp = out_len * 1e6 / denom
     mean = float(tp.sum()) / trials_number

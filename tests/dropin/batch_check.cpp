@@ -19,6 +19,11 @@
 //       throughput of one combination (decoded info bits n - m per trial):
 //         "seam <trials> <seconds> <bits/s>" and "pertrial <trials> <seconds> <bits/s>"
 //       (threads 0: the seam only)
+//   batch_check sweep <matrix> <fmt> <alg> <primary> <secondary> <qbers.txt> <max_it> <trials> <sim_seed>
+//                     [<punctured.txt> <shortened.txt>]
+//       QKD_LDPC_batch_simulation over one combination per QBER (after a
+//       one-combination warm-up), timed as a whole:
+//         "sweep <combinations> <trials> <seconds> <ms per combination> <mean FER>"
 // Failures print "ERROR: <what>" and exit 1.
 #include <atomic>
 #include <chrono>
@@ -244,7 +249,39 @@ int main(int argc, char **argv) {
             std::printf("pertrial %zu %.6f %.6g\n", seeds.size(), s, k * (double)seeds.size() / s);
             return 0;
         }
-        std::fprintf(stderr, "usage: batch_check batch|time ... (see the file header)\n");
+        if (mode == "sweep" && argc >= 11) {
+            set_cfg(argv[4], argv[8], std::strtoull(argv[9], nullptr, 10), std::strtoull(argv[10], nullptr, 10), 0);
+            std::vector<sim_input> in(1);
+            load_into(in[0].matrix, argv[2], std::atoi(argv[3]));
+            in[0].matrix_path = argv[2];
+            const decoding_scaling_factors sf{std::atof(argv[5]), std::atof(argv[6])};
+            H_matrix_params mp;
+            if (argc >= 13) {
+                CFG.ENABLE_CODE_RATE_ADAPTATION = true;
+                mp.punctured_bits = read_int(argv[11]);
+                mp.shortened_bits = read_int(argv[12]);
+            }
+            std::vector<double> qbers;
+            {
+                std::ifstream f(argv[7]);
+                for (double q; f >> q;) qbers.push_back(q);
+            }
+            if (qbers.empty()) throw std::runtime_error("no QBERs");
+            // warm-up: one combination builds the graph, workspaces and buffers
+            in[0].combinations.push_back({qbers[0], mp, sf});
+            (void)QKD_LDPC_batch_simulation(in);
+            in[0].combinations.clear();
+            for (double q : qbers) in[0].combinations.push_back({q, mp, sf});
+            const auto t0 = std::chrono::steady_clock::now();
+            const auto res = QKD_LDPC_batch_simulation(in);
+            const double s = secs_since(t0);
+            double fer = 0.;
+            for (const auto &r : res) fer += 1. - r.ratio_trials_success_ldpc;
+            std::printf("sweep %zu %zu %.6f %.6f %.6g\n", res.size(), (size_t)CFG.TRIALS_NUMBER, s,
+                        1e3 * s / (double)res.size(), fer / (double)res.size());
+            return 0;
+        }
+        std::fprintf(stderr, "usage: batch_check batch|time|sweep ... (see the file header)\n");
         return 2;
     } catch (const std::exception &e) {
         std::printf("ERROR: %s\n", e.what());

@@ -30,11 +30,16 @@ def _rank(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        a, b, q_acc = Q.bsc_frames(64, 0.05, 8, seed=bench.rank_seed(rank))
+        # the slicing bench.main uses for its trials (bench.py: rank_trial_seeds)
+        seeds = bench.rank_trial_seeds(Q, 1022025, 37, world, rank)
         elapsed = 1.0 + rank  # rank 1 is the slow one
         tot = bench.combine_ranks(dist, elapsed, 10 * (rank + 1), 8 - rank, 7, 8, 2.0 * (rank + 1),
                                   torch.device("cpu"))
-        q.put((rank, tot, a.tobytes()))
+        # every rank's slice, gathered over the process group
+        mine = torch.from_numpy(seeds.view(np.int64).copy())
+        got = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        q.put((rank, tot, [g.numpy().view(np.uint64).copy() for g in got]))
     finally:
         dist.destroy_process_group()
 
@@ -55,7 +60,28 @@ def test_two_ranks_combine_and_shard():
     for _, tot, _ in res:  # every rank sees the same global figures
         assert tot["elapsed_max"] == 2.0 and tot["kernel_ms_max"] == 4.0
         assert tot["iters"] == 30 and tot["ok"] == 15 and tot["keys"] == 14 and tot["frames"] == 16
-    assert res[0][2] != res[1][2], "ranks must decode disjoint trials"
+    import qkd_ldpc_v_amd as Q
+
+    full = Q.trial_seeds(1022025, 37 * world)
+    for _, _, slices in res:
+        assert all(sl.size == 37 for sl in slices)
+        # contiguous, complete and in rank order: the concatenation IS the seed list
+        assert np.array_equal(np.concatenate(slices), full)
+    assert len(set(full.tolist())) == full.size, "ranks must decode disjoint trials"
+
+
+def test_rank_trial_seeds_slices():
+    """bench.rank_trial_seeds at world sizes 1..8: rank r's slice is trials
+    [r * batch, (r + 1) * batch) of the reference's seed list."""
+    import bench
+    import qkd_ldpc_v_amd as Q
+
+    for world in (1, 2, 3, 8):
+        full = Q.trial_seeds(1022025, 16 * world)
+        parts = [bench.rank_trial_seeds(Q, 1022025, 16, world, r) for r in range(world)]
+        assert np.array_equal(np.concatenate(parts), full)
+    # rank 0 of a larger job decodes the same first trials as a 1-GPU run
+    assert np.array_equal(bench.rank_trial_seeds(Q, 5555, 64, 8, 0), bench.rank_trial_seeds(Q, 5555, 64, 1, 0))
 
 
 def test_single_rank_combine_without_dist():

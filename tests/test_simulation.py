@@ -271,3 +271,7 @@ def test_throughput_stats_restates_process_trials_results():
     assert lo <= mean <= hi and std > 0
     m2, _, lo2, hi2 = S.throughput_stats(8000, rt, 4, rtt_ms=0.4)
     assert hi2 == int(8000 * 1e6 / (10.0 + 400.0)) and m2 < mean and lo2 < lo
+    # runtimes are whole microseconds (trial_result::runtime), rounded to
+    # nearest and >= 1 — the C++ batch seam's rule (simulation_batch.cpp)
+    assert S.throughput_stats(8000, np.array([9.6, 20.4, 39.5, 80.0]), 4) == (mean, std, lo, hi)
+    assert S.throughput_stats(1000, np.array([0.2]), 1)[2] == int(1000 * 1e6 / 1.0)

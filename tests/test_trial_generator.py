@@ -119,6 +119,81 @@ def test_prefix_shuffle_equals_full_shuffle(n, qber, seed):
     assert np.array_equal(a, pa) and np.array_equal(b, pb)
 
 
+def py_trial_segmented(n, qber, seed, n_punct=0):
+    """The segment-parallel device generator's form (trials.hip): every draw's
+    meaning comes from its index in the trial's stream (Alice's n bits, the
+    shuffle's S draws, the punctured pairs); a shuffle step at a position
+    i < k goes to pbuf[i] and is replayed in order, one at i >= k only
+    contributes a[p] = i for p < k, where the largest i wins (the draw
+    kernel's atomic max); a rejected draw would flag the trial."""
+    g = PyXoshiro(seed)
+    k = int(float(n) * qber)
+    S = n // 2 if n % 2 == 0 else (n - 1) // 2
+    a = [g() >> 63 for _ in range(n)]
+    pbuf = [0] * max(k, 1)
+    last = [0] * max(k, 1)
+    rejected = False
+
+    def record(pos, p):
+        if pos < k:
+            pbuf[pos] = p
+        elif p < k:
+            last[p] = max(last[p], pos)
+
+    for t in range(S):
+        if n % 2 == 0 and t == 0:
+            record(1, g() >> 63)
+            continue
+        i = 2 * t if n % 2 == 0 else 2 * t + 1
+        b1 = i + 2
+        rng = (i + 1) * b1
+        x = g()
+        lo = (x * rng) & M64
+        if lo < rng and lo < ((1 << 64) - rng) % rng:
+            rejected = True
+        hi = (x * rng) >> 64
+        p1 = int(float(hi) / float(b1))  # the kernel's f64 quotient (exact below 2^51)
+        record(i, p1)
+        record(i + 1, hi - p1 * b1)
+    pa, pb = [], []
+    for _ in range(n_punct):
+        pa.append(g() >> 63)
+        pb.append(g() >> 63)
+    pre = list(range(k))
+    for pos in range(1, k):
+        p = pbuf[pos]
+        pre[p], pre[pos] = pos, pre[p]
+    b = list(a)
+    for j in range(k):
+        b[last[j] if last[j] else pre[j]] ^= 1
+    return np.array(a, np.uint8), np.array(b, np.uint8), rejected, pa, pb
+
+
+@pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (2048, 0.0005, 77),
+                                         (1025, 0.3, 9), (10240, 0.013, 1022025), (6, 0.34, 3), (7, 0.15, 1),
+                                         (2, 0.5, 4)])
+def test_segmented_generator_equals_full_shuffle(n, qber, seed):
+    """The segment-parallel generator's prefix replay + last-writer merge gives
+    the full shuffle's keys (no rejection on these streams)."""
+    a, b, _ = py_trial(n, qber, seed)
+    sa, sb, rej, _, _ = py_trial_segmented(n, qber, seed)
+    assert not rej
+    assert np.array_equal(a, sa) and np.array_equal(b, sb)
+
+
+def test_f64_quotient_is_exact_below_2_51():
+    """split_two (trials.hip): floor(fl(x / b1)) == x // b1 for x < 2^51."""
+    rng = np.random.default_rng(5)
+    xs = [int(v) for v in rng.integers(0, 1 << 51, 200000, dtype=np.int64)]
+    bs = [int(v) for v in rng.integers(2, 1 << 26, 200000, dtype=np.int64)]
+    for x, b1 in zip(xs, bs):
+        assert int(float(x) / float(b1)) == x // b1
+    for b1 in (3, 7, 102401, 102402, (1 << 25) + 1):  # quotients just below an integer
+        for q in (1, 12345, (1 << 51) // b1 - 1):
+            x = q * b1 - 1
+            assert int(float(x) / float(b1)) == x // b1
+
+
 @pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (10240, 0.013, 1022025)])
 def test_oracle_trial_matches_python_restatement(n, qber, seed):
     a, b, q = P.trial(n, qber, seed)
@@ -151,7 +226,8 @@ def test_seed_sequences_agree():
 @pytest.mark.parametrize("n,qber,batch", [(1024, 0.013, 24), (1024, 0.0015, 130), (10240, 0.0215, 24),
                                            (10241, 0.05, 24), (102400, 0.038, 4)])
 def test_device_trials_bitexact(gpu_available, n, qber, batch):
-    """(batch 130: three waves of the one-trial-per-lane generator, the last partial)"""
+    """(batch 130: three groups of 64 trials, the last partial; n = 10241 and
+    1024 with batch 24: the byte-store path and a single segment group)"""
     import torch
 
     seeds = Q.trial_seeds(9012025, batch)
@@ -165,6 +241,34 @@ def test_device_trials_bitexact(gpu_available, n, qber, batch):
         a, b, qo = P.trial(n, qber, (int(seeds[f]) + 3) & M64)
         assert np.array_equal(A[f], a) and np.array_equal(B[f], b), f"trial {f} differs"
         assert q == qo
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,qber,batch,n_punct", [(10240, 0.0215, 70, 0), (1023, 0.05, 5, 0), (10240, 0.0156, 9, 37)])
+def test_device_trials_serial_rerun_bitexact(gpu_available, monkeypatch, n, qber, batch, n_punct):
+    """QLDPC_TRIAL_SERIAL=1 sends every trial through the finish kernel's
+    sequential rerun — the path a trial with a rejected shuffle draw takes —
+    which must give the same keys and punctured draws as the oracle."""
+    import torch
+
+    monkeypatch.setenv("QLDPC_TRIAL_SERIAL", "1")
+    seeds = Q.trial_seeds(1022025, batch)
+    d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()
+    da = torch.empty((batch, n), dtype=torch.uint8, device="cuda")
+    db = torch.empty_like(da)
+    if n_punct:
+        pa = torch.empty((batch, n_punct), dtype=torch.uint8, device="cuda")
+        pb = torch.empty_like(pa)
+        Q.trials_rate_adapt_device(n, qber, d_seeds, n_punct, da, db, pa, pb, seed_add=2)
+    else:
+        Q.trials_device(n, qber, d_seeds, da, db, seed_add=2)
+    torch.cuda.synchronize()
+    A, B = da.cpu().numpy(), db.cpu().numpy()
+    for f in range(batch):
+        a, b, _, spa, spb = py_trial_segmented(n, qber, (int(seeds[f]) + 2) & M64, n_punct)
+        assert np.array_equal(A[f], a) and np.array_equal(B[f], b), f"trial {f} differs"
+        if n_punct:
+            assert pa[f].cpu().tolist() == spa and pb[f].cpu().tolist() == spb
 
 
 def test_too_small_for_qber_is_an_error():

@@ -14,7 +14,12 @@ import json, sys
 pts = [json.load(open(f"{sys.argv[1]}/point_{i}.json")) for i in range(26)]
 rows = [{"point": i, "workload": p["config"]["workload"], "gbit_s": p["value"] / 1e9, "ms_per_step": p["ms_per_step"],
          "fer": p["fer"], "mean_iterations": p["mean_iterations"], "info_bits_per_frame": p["config"]["info_bits_per_frame"],
-         "kernel_variant": p["config"]["kernel_variant"], "hbm_frac": p["roofline"]["frac"]} for i, p in enumerate(pts)]
+         "kernel_variant": p["config"]["kernel_variant"],
+         # the line's own algorithmic-byte model ((2E + 2n) * 8 B per frame-iteration / 8 TB/s)
+         "hbm_model_frac": p.get("hbm_model_roofline", p["roofline"])["frac"],
+         # VALU issue fraction only where a PMC pass of THIS point exists (profiles/pmc_c5ra_p<i>.json)
+         "valu_issue_frac": p["compute_roofline"]["frac"] if "compute_roofline" in p else None}
+        for i, p in enumerate(pts)]
 tot_bits = sum(r["gbit_s"] * r["ms_per_step"] for r in rows)
 tot_ms = sum(r["ms_per_step"] for r in rows)
 out = {"sweep": "configs/ADAPTIVE T.json, 26 points, AOMSA, rate-adapted, batch 4096/GPU, 1 GPU", "points": rows,
