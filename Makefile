@@ -34,7 +34,7 @@ $(CSRC)/decoder.o: $(CSRC)/decoder.hip $(CSRC)/decoder_common.hpp $(CSRC)/decode
 $(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/decoder.hpp $(CSRC)/exact_math.h Makefile
 	$(HIPCC) $(HIPFLAGS) $(V2FLAGS) -c $< -o $@
 
-$(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp
+$(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp $(CSRC)/decoder_common.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/order.o: $(CSRC)/order.hip $(CSRC)/decoder.hpp

@@ -329,19 +329,28 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
 }
 
 // ---- QKD_LDPC frame construction (src/qkd_ldpc_algorithm.cpp:1043-1052) --------
+// One workgroup per frame.  Alice's and Bob's keys are first packed into LDS
+// bit words (dev::pack_key_bits: coalesced 16-byte loads), so the palette
+// codes' gather by label (col_orig) and the syndrome's row gathers read LDS.
 __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const int32_t *ell_col,
                                                            const int32_t *row_deg, const uint8_t *alice,
                                                            const uint8_t *bob, const double *log_p,
                                                            double *llr, uint8_t *synd, uint8_t *codes,
                                                            double *palette, uint8_t *pal_ok,
                                                            const int32_t *col_orig) {
+    extern __shared__ uint32_t kb[];
+    const int nw = (n + 31) / 32;
+    uint32_t *abits = kb, *bbits = kb + nw;
     const size_t f = blockIdx.x;
     const double lp = log_p[f];
     const uint8_t *al = alice + f * (size_t)n;
     const uint8_t *bo = bob + f * (size_t)n;
+    dev::pack_key_bits(al, n, abits);
+    dev::pack_key_bits(bo, n, bbits);
+    __syncthreads();
     if (llr) {
         double *l = llr + f * (size_t)n;
-        for (int i = threadIdx.x; i < n; i += blockDim.x) l[i] = bo[i] ? -lp : lp;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) l[i] = dev::key_bit(bbits, i) ? -lp : lp;
     }
     if (codes) {  // V2 palette form: code 0 = +log_p, 1 = -log_p; in label order (col_orig)
         const int nc = (n + 3) / 4;
@@ -350,7 +359,7 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
             int byte = 0;
             for (int s = 0; s < 4; ++s) {
                 const int i = 4 * j + s;
-                if (i < n && bo[col_orig ? col_orig[i] : i]) byte |= 1 << (2 * s);
+                if (i < n && dev::key_bit(bbits, col_orig ? col_orig[i] : i)) byte |= 1 << (2 * s);
             }
             cs[j] = (uint8_t)byte;
         }
@@ -359,10 +368,10 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
     }
     uint8_t *s = synd + f * (size_t)m;
     for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        int p = 0;
+        uint32_t p = 0;
         const int deg = row_deg[j];
-        for (int k = 0; k < deg; ++k) p ^= al[ell_col[(size_t)k * m + j]];
-        s[j] = (uint8_t)(p & 1);
+        for (int k = 0; k < deg; ++k) p ^= dev::key_bit(abits, ell_col[(size_t)k * m + j]);
+        s[j] = (uint8_t)p;
     }
 }
 
@@ -465,7 +474,14 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                const int32_t *col_orig, hipStream_t stream) {
     (void)max_dc;
     if (batch <= 0) return hipSuccess;
-    hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, alice,
+    const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);  // the two keys as bit words
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(build_frames_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, alice,
                        bob, log_p, llr, synd, codes, palette, pal_ok, col_orig);
     return hipGetLastError();
 }

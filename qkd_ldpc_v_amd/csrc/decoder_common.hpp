@@ -21,6 +21,32 @@
 namespace qldpc {
 namespace dev {
 
+// A frame's key bytes (0 / 1 each) packed into LDS bit words by the whole
+// workgroup: word w holds bits 32 w .. 32 w + 31.  With n % 32 == 0 and a
+// 16-byte aligned key, each word is two 16-byte loads (a wave reads 2 KiB
+// contiguously); otherwise byte loads.  The frame builders then gather key
+// bits from LDS instead of bytes from L2.
+__device__ __forceinline__ uint32_t pack4(uint32_t x) {  // 4 bytes of 0 / 1 -> 4 bits
+    return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
+}
+__device__ inline void pack_key_bits(const uint8_t *key, int n, uint32_t *bits) {
+    const int nw = (n + 31) / 32;
+    const bool wide = (n % 32 == 0) && ((reinterpret_cast<uintptr_t>(key) & 15) == 0);
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+        uint32_t v = 0;
+        if (wide) {
+            const uint4 *k4 = reinterpret_cast<const uint4 *>(key) + 2 * w;
+            const uint4 lo = k4[0], hi = k4[1];
+            v = pack4(lo.x) | (pack4(lo.y) << 4) | (pack4(lo.z) << 8) | (pack4(lo.w) << 12) | (pack4(hi.x) << 16) |
+                (pack4(hi.y) << 20) | (pack4(hi.z) << 24) | (pack4(hi.w) << 28);
+        } else {
+            for (int b = 0; b < 32 && 32 * w + b < n; ++b) v |= (uint32_t)(key[32 * w + b] & 1u) << b;
+        }
+        bits[w] = v;
+    }
+}
+__device__ __forceinline__ uint32_t key_bit(const uint32_t *bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1u; }
+
 // threshold_matrix (src/array_and_matrix_operations.cpp:953-972): v > thr -> thr,
 // v < -thr -> -thr, NaN passes.  With thr > 0 that is |v| > thr -> copysign(thr, v):
 // one compare (abs modifier), one bfi and two selects.

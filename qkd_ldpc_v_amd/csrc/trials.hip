@@ -44,6 +44,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "decoder_common.hpp"
+
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
@@ -154,8 +156,18 @@ __global__ void __launch_bounds__(64) trials_draw_kernel(int n, uint32_t k, int 
     uint64_t d = seg * kSeg;
     const uint64_t d1 = (d + kSeg < T.D) ? d + kSeg : T.D;
     Xoshiro256pp g((act ? seeds[f] : 0ull) + seed_add);
-    if (seg > 0) {  // the state at draw seg * kSeg: J · s over GF(2), columns by wave-uniform loads
-        const uint64_t *J = jt + seg * 1024;
+    if (seg > 0) {  // the state at draw seg * kSeg: J · s over GF(2)
+        // the segment's matrix (8 KiB) staged in LDS by one coalesced load round
+        // (eight 16-byte loads per lane in flight), then its columns read by
+        // broadcast LDS reads
+        __shared__ uint4 jl[512];
+        const uint4 *J4 = reinterpret_cast<const uint4 *>(jt + seg * 1024);
+        uint4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = J4[q * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) jl[q * 64 + lane] = v[q];
+        __syncthreads();
         const uint64_t st[4] = {g.s0, g.s1, g.s2, g.s3};
         uint64_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
 #pragma unroll
@@ -164,11 +176,11 @@ __global__ void __launch_bounds__(64) trials_draw_kernel(int n, uint32_t k, int 
 #pragma unroll 8
             for (int b = 0; b < 64; ++b) {
                 const uint64_t m = 0ull - ((sw >> b) & 1ull);
-                const uint64_t *c = J + 4 * (64 * w + b);
-                r0 ^= c[0] & m;
-                r1 ^= c[1] & m;
-                r2 ^= c[2] & m;
-                r3 ^= c[3] & m;
+                const uint4 c01 = jl[2 * (64 * w + b)], c23 = jl[2 * (64 * w + b) + 1];
+                r0 ^= (((uint64_t)c01.y << 32) | c01.x) & m;
+                r1 ^= (((uint64_t)c01.w << 32) | c01.z) & m;
+                r2 ^= (((uint64_t)c23.y << 32) | c23.x) & m;
+                r3 ^= (((uint64_t)c23.w << 32) | c23.z) & m;
             }
         }
         g.s0 = r0;
@@ -337,7 +349,9 @@ __global__ void __launch_bounds__(256) trials_finish_kernel(int n, uint32_t k, i
 // shortened bit (cls 2: 0 on both sides, LLR DBL_MAX); src[i] indexes the key
 // or punctured draw.  Writes Alice's extended key, optionally the LLRs, the
 // V2 palette form (codes 0/1 = +-log_p, 2 = 1e-4, 3 = DBL_MAX) and the Alice
-// syndrome of the extended key.
+// syndrome of the extended key.  One workgroup per frame; the keys, the
+// punctured draws and the extended key live in LDS as bit words, so every
+// gather (by src, by label, by row) reads LDS.
 __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, const int32_t *ell_col,
                                                               const int32_t *row_deg, const uint8_t *cls,
                                                               const int32_t *src, int n_punct,
@@ -346,21 +360,40 @@ __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, cons
                                                               const double *log_p, uint8_t *alice_ext, double *llr,
                                                               uint8_t *synd, uint8_t *codes, double *palette,
                                                               uint8_t *pal_ok, const int32_t *col_orig) {
+    extern __shared__ uint32_t kb[];
+    const int nw = (n + 31) / 32, pw = (n_punct + 31) / 32, xw = 2 * ((n + 63) / 64);
+    uint32_t *abits = kb, *bbits = kb + nw, *pbits = kb + 2 * nw, *xbits = kb + 2 * nw + pw;
     const size_t f = blockIdx.x;
     const double lp = log_p[f];
-    const uint8_t *al = alice + f * (size_t)n;
-    const uint8_t *bo = bob + f * (size_t)n;
-    const uint8_t *pa = palice + f * (size_t)n_punct;
     (void)pbob;  // Bob's punctured draws only advance the generator (LLR = ALMOST_ZERO)
-    uint8_t *ax = alice_ext + f * (size_t)n;
+    dev::pack_key_bits(alice + f * (size_t)n, n, abits);
+    dev::pack_key_bits(bob + f * (size_t)n, n, bbits);
+    if (n_punct > 0) dev::pack_key_bits(palice + f * (size_t)n_punct, n_punct, pbits);
+    __syncthreads();
+    // the extended Alice key, 64 positions per wave ballot
+    const int lane = threadIdx.x & 63;
+    for (int base = (int)(threadIdx.x & ~63u); base < 32 * xw; base += blockDim.x) {
+        const int i = base + lane;
+        uint32_t bit = 0;
+        if (i < n) {
+            const int c = cls[i];
+            bit = c == 0 ? dev::key_bit(abits, src[i]) : (c == 1 ? dev::key_bit(pbits, src[i]) : 0u);
+        }
+        const uint64_t bal = __ballot(bit);
+        if (lane == 0) {
+            xbits[base >> 5] = (uint32_t)bal;
+            xbits[(base >> 5) + 1] = (uint32_t)(bal >> 32);
+        }
+    }
+    __syncthreads();
     auto bob_code = [&](int i) -> int {  // palette code of position i
         const int c = cls[i];
-        if (c == 0) return bo[src[i]] ? 1 : 0;
+        if (c == 0) return (int)dev::key_bit(bbits, src[i]);
         return c == 1 ? 2 : 3;
     };
+    uint8_t *ax = alice_ext + f * (size_t)n;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int c = cls[i];
-        ax[i] = c == 0 ? al[src[i]] : (c == 1 ? pa[src[i]] : 0);
+        ax[i] = (uint8_t)dev::key_bit(xbits, i);
         if (llr) {
             const int code = bob_code(i);
             llr[f * (size_t)n + i] = code == 0 ? lp : code == 1 ? -lp : code == 2 ? 1e-4 : 1.7976931348623157e308;
@@ -383,13 +416,12 @@ __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, cons
         }
         if (threadIdx.x == 0) pal_ok[f] = 1;
     }
-    __syncthreads();  // the extended key is complete (global, this block)
     uint8_t *s = synd + f * (size_t)m;
     for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        int p = 0;
+        uint32_t p = 0;
         const int deg = row_deg[j];
-        for (int k = 0; k < deg; ++k) p ^= ax[ell_col[(size_t)k * m + j]];
-        s[j] = (uint8_t)(p & 1);
+        for (int k = 0; k < deg; ++k) p ^= dev::key_bit(xbits, ell_col[(size_t)k * m + j]);
+        s[j] = (uint8_t)p;
     }
 }
 
@@ -401,8 +433,17 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
                                   double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,
                                   const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), 0, stream, n, m, ell_col, row_deg, cls, src,
-                       n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok,
+    // LDS: Alice's and Bob's keys, the punctured draws and the extended key as bit words
+    const size_t lds = (2 * (size_t)((n + 31) / 32) + (size_t)((n_punct + 31) / 32) + 2 * (size_t)((n + 63) / 64)) *
+                       sizeof(uint32_t);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(build_frames_ra_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, cls,
+                       src, n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok,
                        col_orig);
     return hipGetLastError();
 }

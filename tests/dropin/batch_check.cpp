@@ -22,7 +22,7 @@
 //   batch_check sweep <matrix> <fmt> <alg> <primary> <secondary> <qbers.txt> <max_it> <trials> <sim_seed>
 //                     [<punctured.txt> <shortened.txt>]
 //       QKD_LDPC_batch_simulation over one combination per QBER (after a
-//       one-combination warm-up), timed as a whole:
+//       two-combination warm-up), timed as a whole:
 //         "sweep <combinations> <trials> <seconds> <ms per combination> <mean FER>"
 // Failures print "ERROR: <what>" and exit 1.
 #include <atomic>
@@ -237,7 +237,9 @@ int main(int argc, char **argv) {
             // warm-up: the graph, the device workspaces and the pinned buffers
             // are built by the first call of a size (as in the reference's loop,
             // every later combination reuses them)
+            // (twice: consecutive calls alternate over a device's two pipeline slots)
             qkd_ldpc_hip_run_trials(H, qber, seeds, 1, {}, sf, tr);
+            qkd_ldpc_hip_run_trials(H, qber, seeds, 2, {}, sf, tr);
             auto t0 = std::chrono::steady_clock::now();
             qkd_ldpc_hip_run_trials(H, qber, seeds, 0, {}, sf, tr);
             double s = secs_since(t0);
@@ -267,7 +269,9 @@ int main(int argc, char **argv) {
                 for (double q; f >> q;) qbers.push_back(q);
             }
             if (qbers.empty()) throw std::runtime_error("no QBERs");
-            // warm-up: one combination builds the graph, workspaces and buffers
+            // warm-up: two combinations build the graph, the workspaces and both
+            // pipeline slots' buffers
+            in[0].combinations.push_back({qbers[0], mp, sf});
             in[0].combinations.push_back({qbers[0], mp, sf});
             (void)QKD_LDPC_batch_simulation(in);
             in[0].combinations.clear();

@@ -6,9 +6,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 O=gpurun_out/r05_gen; mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_trial_generator.py tests/test_run_trials.py tests/test_dropin.py tests/test_simulation.py \
-  tests/test_rate_adapt.py tests/test_multi.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 10; }
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ \
+  > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 10; }
 tail -3 $O/pytest.log
 for w in c2 c4 c4g c5ra; do
   timeout -k 10 300 python bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_$w.json 2> $O/bench_$w.err || { tail -5 $O/bench_$w.err; exit 11; }
@@ -28,3 +27,6 @@ M4=tests/golden/matrices/c4s_n102400_m32001.alist.gz
 printf '0.038\n0.038\n0.038\n0.038\n' > $O/q_c4.txt
 timeout -k 10 240 tests/dropin/batch_check sweep $M4 1 0 0 0 $O/q_c4.txt 50 128 1022025 > $O/sweep_c4.txt 2>&1 || { cat $O/sweep_c4.txt; exit 15; }
 echo "sweep c4: $(cat $O/sweep_c4.txt)"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o seam -- tests/dropin/batch_check time $M 1 0 0 0 0.0215 50 4096 1022025 0 > $O/seam_prof.txt 2>&1 || { tail -20 $O/seam_prof.txt; exit 16; }
+find $O/prof -name "*stats*"
