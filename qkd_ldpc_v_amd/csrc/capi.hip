@@ -121,10 +121,6 @@ struct DeviceGraph {
     int32_t *row_orig = nullptr;  // V2: layout row -> original row (syndrome index)
     int32_t *part_row0 = nullptr; // V2 split: first layout row of each part
     int32_t *xoff = nullptr;      // V2 split exchange: region starts
-    int32_t *pbits = nullptr, *pbits_off = nullptr;  // V2 split local totals: per part its bits
-    std::mutex xcd_mu;                // K = 32 split launches: serialised on the device (xcd_ev)
-    hipEvent_t xcd_ev = nullptr;
-    bool xcd_recorded = false;
     uint16_t *xbit = nullptr, *xbit_ms = nullptr;  // ... chunk-local bit per stage position (CSR / kpos layouts)
     int32_t *iso_bits = nullptr;
     uint32_t *vn_rows = nullptr;  // V2 min-sum bit gather: [n or chunks][2] four u16 layout rows
@@ -209,9 +205,6 @@ struct qldpc_graph {
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
     int split_cb = 0, split_nc = 0;         // V2 split exchange gather: bits per LDS chunk, chunks per part (0: off)
-    bool split_local = false;               // V2 split over a whole XCD, each part's totals in LDS
-    int split_nloc = 0;                     // ... the largest part's bit list (LDS entries)
-    std::vector<int32_t> pbits, pbits_off;  // ... per part: its sorted bits + the dummy column n
     bool kernel_timing = false;             // qldpc_set_kernel_timing
     std::vector<int32_t> col_lab;           // V2 bank relabelling (relabel.cpp): bit id -> label; empty: identity
     long long relabel_stats[4] = {0, 0, 0, 0};  // bank excess before / after, busiest-bank cycles before / after
@@ -237,8 +230,7 @@ int block_threads(const qldpc_graph &g) {
 
 size_t lds_of(const qldpc_graph &g, int alg) {
     if (g.variant == VAR_V2 && g.split_k > 1)
-        return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true, g.split_local ? V2_R_LOCAL : 0, 0, -1, g.split_cb,
-                            g.split_local ? g.split_nloc : 0);
+        return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true, 0, 0, -1, g.split_cb);
     return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG,
                                               (g.rows_global_ms && alg >= 2) ? g.rows_lds_ms : -1)
                                : lds_bytes_for(g.variant, g.n, g.m, g.T);
@@ -484,9 +476,6 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
 // XCD's 32 CUs), rows dealt to the 16K waves as in plan_v2 (contiguous
 // balanced blocks), part r = waves [16r, 16r + 16).  Totals go to global
 // memory.  QLDPC_SPLIT=0 disables it (v1 is used).
-#ifndef QL_SPLIT_LOCAL_DEFAULT
-#define QL_SPLIT_LOCAL_DEFAULT 0
-#endif
 bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_idx) {
     if (env_int("QLDPC_SPLIT", 1) == 0) return false;
     if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
@@ -494,9 +483,8 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         if (row_ptr[j + 1] == row_ptr[j]) return false;
     const long long E = g.E;
     const int WP = REG_TSTRIDE / 64;
-    // One attempt: K parts of R slots per lane; local = the part's totals in
-    // LDS (K = 32, V2_R_LOCAL: decoder_v2.hip LOCAL).
-    auto attempt = [&](int K, int R, bool local) -> bool {
+    // One attempt: K parts of R slots per lane.
+    auto attempt = [&](int K, int R) -> bool {
         const int W = WP * K;
         const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
         if (cap > 64LL * R) return false;
@@ -530,41 +518,20 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         int mrows = 0;
         for (int r = 0; r <= K; ++r) prow[r] = rb[std::min(W, r * WP)];
         for (int r = 0; r < K; ++r) mrows = std::max(mrows, prow[r + 1] - prow[r]);
-        // local totals: per part the sorted bits its rows touch, then the dummy column n
-        std::vector<int32_t> pbits, poff(1, 0);
-        int nloc = 0;
-        if (local) {
-            std::vector<int> mark(g.n, -1);
-            for (int r = 0; r < K; ++r) {
-                const size_t b0 = pbits.size();
-                for (int j = prow[r]; j < prow[r + 1]; ++j)
-                    for (int e = row_ptr[order[j]]; e < row_ptr[order[j] + 1]; ++e)
-                        if (mark[col_idx[e]] != r) {
-                            mark[col_idx[e]] = r;
-                            pbits.push_back(col_idx[e]);
-                        }
-                std::sort(pbits.begin() + (long)b0, pbits.end());
-                pbits.push_back(g.n);
-                poff.push_back((int32_t)pbits.size());
-                nloc = std::max(nloc, (int)(pbits.size() - b0));
-            }
-            if (nloc > 0xFFFF) return false;  // local indices are 16-bit (col_off8)
-        }
-        const int Rk = local ? V2_R_LOCAL : 0;
-        if (lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, Rk, 0, -1, 0, nloc) > LDS_LIMIT ||
-            lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, Rk, 0, -1, 0, nloc) > LDS_LIMIT)
+        if (lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, 0) > LDS_LIMIT ||
+            lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, 0) > LDS_LIMIT)
             return false;
         // Exchange gather (DecodeArgs::xoff): the largest LDS chunk of a part's
         // bits every algorithm's layout holds (SPA keeps its LDS message slots
         // when they fit without it), split evenly; QLDPC_SPLIT_X=0: the
-        // term-major stage (A/B; not with local totals).
+        // term-major stage (A/B).
         int cb = 0, nc = 0;
-        if (local || env_int("QLDPC_SPLIT_X", 1)) {
+        if (env_int("QLDPC_SPLIT_X", 1)) {
             const int own = (g.n + K - 1) / K;
-            const bool rl0 = !local && v2_split_rl_fits(g.n, mrows, 0);
+            const bool rl0 = v2_split_rl_fits(g.n, mrows, 0);
             auto fits = [&](int c) {
-                return lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, Rk, 0, -1, c, nloc) <= LDS_LIMIT &&
-                       lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, Rk, 0, -1, c, nloc) <= LDS_LIMIT &&
+                return lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, c) <= LDS_LIMIT &&
+                       lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, c) <= LDS_LIMIT &&
                        (!rl0 || v2_split_rl_fits(g.n, mrows, c));
             };
             int lo = 0, hi = std::min(own, 0xFFFF);
@@ -576,12 +543,10 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
             if (lo >= 256) {
                 nc = (own + lo - 1) / lo;
                 cb = (own + nc - 1) / nc;
-            } else if (local) {
-                return false;
             }
         }
         g.variant = VAR_V2;
-        g.v2R = local ? V2_R_LOCAL : R;
+        g.v2R = R;
         g.v2RG = 0;
         g.T = W * 64;
         g.EPL = epl;
@@ -593,10 +558,6 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         g.part_row0 = prow;
         g.split_cb = cb;
         g.split_nc = nc;
-        g.split_local = local;
-        g.split_nloc = nloc;
-        g.pbits = std::move(pbits);
-        g.pbits_off = std::move(poff);
         return true;
     };
     // QLDPC_SPLIT_K forces the part count (<= 32: one XCD's CUs)
@@ -604,13 +565,10 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
     const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
     if (kforce && (kforce < kmin || kforce > 32)) return false;
-    // A frame over a whole XCD with its parts' totals in LDS when the code
-    // allows it (QLDPC_SPLIT_LOCAL=0: the 16-wave parts below, A/B)
-    if (!kforce && env_int("QLDPC_SPLIT_LOCAL", QL_SPLIT_LOCAL_DEFAULT) && attempt(32, V2_R_LOCAL, true)) return true;
     // (K need not divide an XCD's 32 workgroups: groups form in claim order and
     // a workgroup joins the next group whenever it finishes a frame)
     for (int K = kforce ? kforce : kmin; K <= (kforce ? kforce : 16); ++K)
-        if (attempt(K, V2_R_TIGHT, false)) return true;
+        if (attempt(K, V2_R_TIGHT)) return true;
     return false;
 }
 
@@ -1154,27 +1112,6 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         assign(meta, meta2, xbit);
         assign(meta_ms, meta2_ms, xbit_ms);
     }
-    // Local totals (plan_v2_split, K = 32): the scan of part p reads its bits'
-    // totals from LDS, so the metadata's bit field becomes the index into the
-    // part's sorted bit list (the dummy column n is its last entry).  After the
-    // exchange positions, which are assigned by global bit.
-    if (v2 && g->split_local) {
-        auto localize = [&](std::vector<uint32_t> &mt) -> bool {
-            for (int l = 0; l < T; ++l) {
-                const int p = l / REG_TSTRIDE;
-                const int32_t *b0 = g->pbits.data() + g->pbits_off[p], *b1 = g->pbits.data() + g->pbits_off[p + 1];
-                for (int k = 0; k < S4; ++k) {
-                    uint32_t &w = mt[midx(l, k)];
-                    const int32_t c = (int32_t)(w & META_COL_MASK);
-                    const int32_t *it = std::lower_bound(b0, b1, c);
-                    if (it == b1 || *it != c) return false;
-                    w = (w & ~META_COL_MASK) | (uint32_t)(it - b0);
-                }
-            }
-            return true;
-        };
-        if (!localize(meta) || !localize(meta_ms)) return fail(QLDPC_EUNSUP, "split local totals: bit list");
-    }
     g->nst_max = row_sem.empty() ? 0 : nst_max;
     if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
         auto visited = [&](const std::vector<uint64_t> &v) {
@@ -1250,7 +1187,6 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
             (rc = upload(&dg->stage_off, stage_off)) || (rc = upload(&dg->row_orig, row_orig)) ||
             (rc = upload(&dg->part_row0, g->part_row0)) || (rc = upload(&dg->xoff, xoff)) ||
             (rc = upload(&dg->xbit, xbit)) || (rc = upload(&dg->xbit_ms, xbit_ms)) ||
-            (rc = upload(&dg->pbits, g->pbits)) || (rc = upload(&dg->pbits_off, g->pbits_off)) ||
             (rc = upload(&dg->lane_row0, lrow0)) || (rc = upload(&dg->wave_rows, g->wave_rows)) ||
             (rc = upload(&dg->lane_head, lhead)) || (rc = upload(&dg->lane_nst, lnst)) ||
             (rc = upload(&dg->lane_epl, lepl)) || (rc = upload(&dg->ell_col, ell)) ||
@@ -1492,9 +1428,6 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         a.split_nc = g->split_nc;
         a.xoff = g->split_cb > 0 ? dg->xoff : nullptr;
         a.xbit = alg >= 2 ? dg->xbit_ms : dg->xbit;
-        a.split_nloc = g->split_local ? g->split_nloc : 0;
-        a.pbits = dg->pbits;
-        a.pbits_off = dg->pbits_off;
         HIP_TRY(hipMemsetAsync(w->split_ctl, 0, (32 + 3 * 16 * (size_t)slots) * sizeof(int), stream));
     }
     a.nc = (g->n + 3) / 4;
@@ -1540,15 +1473,6 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
     a.stamps = d_st;
 #endif
-    // A K = 32 split launch needs every CU of an XCD for one part group: two in
-    // flight on different streams could each hold part of an XCD and never
-    // form a group, so such launches are serialised on the device.
-    std::unique_lock<std::mutex> xcd_lk;
-    if (v2 && g->split_local) {
-        xcd_lk = std::unique_lock<std::mutex>(dg->xcd_mu);
-        if (!dg->xcd_ev) HIP_TRY(hipEventCreateWithFlags(&dg->xcd_ev, hipEventDisableTiming));
-        if (dg->xcd_recorded) HIP_TRY(hipStreamWaitEvent(stream, dg->xcd_ev, 0));
-    }
     if (g->kernel_timing) {  // (the workspace is per stream: no other call records on these events)
         if (!w->ev0) HIP_TRY(hipEventCreate(&w->ev0));
         if (!w->ev1) HIP_TRY(hipEventCreate(&w->ev1));
@@ -1556,11 +1480,6 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     }
     if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
     else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
-    if (xcd_lk.owns_lock()) {
-        HIP_TRY(hipEventRecord(dg->xcd_ev, stream));
-        dg->xcd_recorded = true;
-        xcd_lk.unlock();
-    }
     if (g->kernel_timing) {
         HIP_TRY(hipEventRecord(w->ev1, stream));
         w->ev_recorded = true;
@@ -1776,9 +1695,6 @@ void qldpc_graph_destroy(qldpc_graph *g) {
         (void)hipFree(d->xoff);
         (void)hipFree(d->xbit);
         (void)hipFree(d->xbit_ms);
-        (void)hipFree(d->pbits);
-        (void)hipFree(d->pbits_off);
-        if (d->xcd_ev) (void)hipEventDestroy(d->xcd_ev);
         (void)hipFree(d->vn_mask);
         (void)hipFree(d->vn_mask_ms);
         (void)hipFree(d->vn_exec);

@@ -31,9 +31,6 @@ enum Variant : int {
 // waves, holds no more edges than 56 x 12 and its SPA build falls back to a
 // scratch array, so it is not built.)
 constexpr int V2_R_TIGHT = 40, V2_R_SMALL = 44, V2_R_MID = 56;
-// Split frames over a whole XCD (K = 32 parts, <= 24 slots per lane): each
-// part keeps the totals of the bits its rows touch in LDS (DecodeArgs::pbits).
-constexpr int V2_R_LOCAL = 24;
 constexpr int V2_CODES_CAP = 20480;  // V2: bits per frame whose palette indices fit LDS (n <= this)
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;
@@ -136,14 +133,6 @@ struct DecodeArgs {
     int split_cb, split_nc;
     const int32_t *xoff;            // [K * nc * dv_max + 1] region starts (doubles into the frame's stage)
     const uint16_t *xbit;           // [stage_frame_doubles] chunk-local bit of each stage position
-    // Local totals (V2_R_LOCAL split instantiation): part p's slot metadata
-    // carries local bit indices into pbits[pbits_off[p] ..], the sorted bits
-    // its rows touch plus the dummy column n (last); the part refreshes their
-    // totals into LDS after every group barrier that follows the gather, and
-    // its scan reads LDS.  split_nloc: the largest list (LDS entries).
-    int split_nloc;
-    const int32_t *pbits;
-    const int32_t *pbits_off;       // [split_k + 1]
     // v1 global-slot kernels, unsorted adjacency (occurrence pairing): input
     // slot s of the next check-node pass gets total[pair_col[s]] -
     // c2b[pair_src[s]] (both [k][lane]); the values go through a slot-major
@@ -213,7 +202,7 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
 // LDS bytes of a V2 launch; R/RG select the shape (whether message slots live in LDS).
 // rows_lds: min-sum row aggregates kept in LDS on the hybrid shape (-1: all m).
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0, int RG = 0, int rows_lds = -1,
-                    int gcb = 0, int nloc = 0);
+                    int gcb = 0);
 // Whether a V2 shape can run the min-sum bit gather (DecodeArgs::vn_rows):
 // the dv <= 4 register shape, or the hybrid shape when the padded edge
 // positions' two code bits fit the LDS byte area.

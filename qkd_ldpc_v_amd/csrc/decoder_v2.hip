@@ -71,9 +71,9 @@ constexpr int V2_A0_ENTRIES = 64;
 // memory and the palette indices are read from the 2-bit global codes; LDS
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
-    size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, ltot, codes, palette, syn, bytes;
+    size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, syn, bytes;
     __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0,
-                                 bool rowscan = false, int gcb = 0, int nloc = 0) {
+                                 bool rowscan = false, int gcb = 0) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
@@ -88,7 +88,6 @@ struct V2Layout {
         if (split && gcb > 0 && al16(rows + (size_t)gcb * 8) > o) o = al16(rows + (size_t)gcb * 8);
         ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * (sizeof(ql_exact::Expm1A) + sizeof(ql_exact::Expm1B))));  // SPA: tanh's expm1 classes
         msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
-        ltot = o; o = al16(o + (size_t)nloc * 8);             // split, local totals: the part's bits
         // one workgroup per frame: the rows' target syndrome bits as sign words
         // (s << 31), in the palette-index area past the codes when it has room
         syn = 0;
@@ -143,8 +142,7 @@ __device__ __forceinline__ void st_row16(__amdgpu_buffer_rsrc_t rs, int r, doubl
 template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN, int R>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT)
-        return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL, false, a.split_cb,
-                        R == V2_R_LOCAL ? a.split_nloc : 0);
+        return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL, false, a.split_cb);
     else return V2Layout(a.n, RGLB ? a.rows_lds : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
@@ -235,9 +233,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     // goes on (sign flips commute with round-to-nearest); min-sum rows get
     // their sign at END and (ANMSA/AOMSA) their mismatch flag after the loop.
     constexpr bool ROWSCAN = V2_ROWSCAN_ON && !SPLIT && RG == 0;
-    // Split frames over a whole XCD: the part's totals in LDS (DecodeArgs::pbits)
-    constexpr bool LOCAL = SPLIT && R == V2_R_LOCAL;
-    static_assert(!LOCAL || RL == 0, "local totals: no LDS message slots");
 
     const int tid = threadIdx.x;
     const int T = a.T, n = a.n, m = a.m, nc = a.nc;
@@ -287,9 +282,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     uint8_t *codes = smem + V2_CODES_OFF;
     // total[bit id of metadata word mt] (LDS totals: by col_off8)
     const uint32_t total_lds = (uint32_t)(uintptr_t)(lds_f64 *)(smem + V2_TOTAL_OFF);
-    // LOCAL: the part's totals, by the local bit index in the metadata word
-    double *const ltot = reinterpret_cast<double *>(smem + L.ltot);
-    const uint32_t ltot_lds = (uint32_t)(uintptr_t)(lds_f64 *)(smem + L.ltot);
     auto tot_at = [&](uint32_t mt) -> auto & {
         if constexpr (!SPLIT) return *col_off8(mt, total_lds);
         else return total[(int)(mt & META_COL_MASK)];
@@ -524,26 +516,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         STAMP(ST_SETUP);
         psync();
         STAMP(ST_SETUP_WAIT);
-        // LOCAL: copy the totals of the part's bits into LDS — after a group
-        // barrier (the frame's totals are then complete and re-read past L1),
-        // four independent loads per thread in flight.
-        auto refresh_local = [&]() {
-            if constexpr (LOCAL) {
-                const int off = a.pbits_off[rank];
-                const int cnt = a.pbits_off[rank + 1] - off;
-                for (int j0 = tid; j0 < cnt; j0 += 4 * T) {
-                    double v[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (j0 + q * T < cnt) v[q] = total[a.pbits[off + j0 + q * T]];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (j0 + q * T < cnt) ltot[j0 + q * T] = v[q];
-                }
-                __syncthreads();
-            }
-        };
-        refresh_local();
 
         int iters = a.max_it, okv = 0;
         bool had_vn = false;
@@ -914,7 +886,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             uint32_t zt = 0;
             meta.each_upto(epl, [&](int k, uint32_t mt) {
                 const int col = (int)(mt & META_COL_MASK);
-                const double tv = LOCAL ? (double)*col_off8(mt, ltot_lds) : total[col];
+                const double tv = total[col];
                 const int zb = (tv <= 0.0) ? 1 : 0;
                 if (k < KT) zt |= (uint32_t)zb << k;
                 const bool start = (mt & META_START) != 0;
@@ -953,7 +925,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             it0 = 1;
         }
         for (int it = it0;; ++it) {
-            if (had_vn) refresh_local();  // (LOCAL: the gather rewrote the totals)
             // SPA: iteration 0's b2c is the unclipped channel LLR (:21-29)
             const double lim_it = had_vn ? lim : 44.0;
             const double tlim_it = had_vn ? a.spa_tlim : 1.0;  // tanh(22) = 1
@@ -1171,11 +1142,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
             };
             if constexpr (SPLIT) {  // totals in global memory: a group's four loads issued together
-                if constexpr (LOCAL) {  // totals in LDS: no group of global loads to cover
-                    meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, (double)*col_off8(mt, ltot_lds)); });
-                } else {
-                    meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
-                }
+                meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, tot_at(mt)); });
             }
@@ -1467,7 +1434,6 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
 }
 
 KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
-    if (split_k > 1 && R == V2_R_LOCAL) return pick_v2<V2_R_LOCAL, 0, true>(alg);
     if (split_k > 1) {
         if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT>
                                 : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT>;
@@ -1482,9 +1448,7 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 
 }  // namespace
 
-size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds, int gcb, int nloc) {
-    if (split && R == V2_R_LOCAL)  // local totals: no LDS message slots
-        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, 0, false, gcb, nloc).bytes;
+size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds, int gcb) {
     if (split)
         return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb) ? V2_RL_SPLIT : 0,
                         false, gcb)
@@ -1517,8 +1481,7 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
-                                       a.split_k > 1 ? (a.v2R != V2_R_LOCAL &&
-                                                        v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb))
+                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb)
                                                      : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);

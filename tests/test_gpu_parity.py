@@ -339,40 +339,20 @@ def test_c4_generated_dv4_ten_parts(gpu_available, alg, prim, sec):
         assert bits_equal_nan(out.posterior[f], op[f])
 
 
-@pytest.mark.parametrize("alg,prim,sec", ALGS)
-def test_c4_100k_split_local_totals(gpu_available, monkeypatch, alg, prim, sec):
-    """QLDPC_SPLIT_LOCAL=1 (read when the graph is created): a frame over the
-    32 workgroups of one XCD, each part's totals in LDS (decoder_v2.hip
-    LOCAL, DecodeArgs::pbits) — bit-exact with the oracle, posteriors included."""
-    H = load_fixture("c4s_n102400_m32001.alist")
-    monkeypatch.setenv("QLDPC_SPLIT_LOCAL", "1")
-    g = Q.Graph(H)
-    monkeypatch.delenv("QLDPC_SPLIT_LOCAL")
-    assert g.plan(0, alg)["lanes"] == 32 * 1024
-    _, _, llr, synd = frames(H, 0.038, 10, 140 + alg)
-    out = g.decode(Q.Params(alg, 8, True, 100.0, prim, sec), llr, synd, posterior=True)
-    O = Oracle(H)
-    ob, oi, ok, op = O.decode_batch(O.params(alg, 8, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
-    for f in range(llr.shape[0]):
-        assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
-        assert bits_equal_nan(out.posterior[f], op[f])
-
-
-@pytest.mark.parametrize("env", [{"QLDPC_SPLIT_LOCAL": "0"}, {"QLDPC_SPLIT_LOCAL": "0", "QLDPC_SPLIT_X": "0"}])
+@pytest.mark.parametrize("env", [{"QLDPC_SPLIT_X": "0"}, {"QLDPC_SPLIT_K": "10"}])
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0)])
 def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec, env):
     """The split layouts other than the default (read when the graph is
-    created): 16-wave parts with global totals (QLDPC_SPLIT_LOCAL=0, K = 8)
-    with the exchange stage, and with the term-major stage (QLDPC_SPLIT_X=0,
-    the A/B arm of DecodeArgs::xoff) — same bits, iterations and posteriors as
-    the oracle and as the default graph."""
+    created): the term-major stage (QLDPC_SPLIT_X=0, the A/B arm of
+    DecodeArgs::xoff) and K = 10 parts instead of the planner's 8 — same
+    bits, iterations and posteriors as the oracle and as the default graph."""
     H = load_fixture("c4s_n102400_m32001.alist")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g0 = Q.Graph(H)
     for k in env:
         monkeypatch.delenv(k)
-    assert g0.plan(0, alg)["lanes"] == 8 * 1024
+    assert g0.plan(0, alg)["lanes"] == int(env.get("QLDPC_SPLIT_K", 8)) * 1024
     _, _, llr, synd = frames(H, 0.038, 6, 90 + alg)
     p = Q.Params(alg, 10, True, 100.0, prim, sec)
     out0 = g0.decode(p, llr, synd, posterior=True)
