@@ -17,12 +17,14 @@
 // generator outputs (S = the shuffle's draws: n/2 for even n, (n-1)/2 for odd
 // n).  Xoshiro256's state transition is linear over GF(2), so the state at
 // draw d is J_d · s (J_d = M^d, a 256 x 256 bit matrix): the stream is cut
-// into segments of kSeg draws and every segment starts from J_{j kSeg} · s
-// (a host-built table, one matrix per segment index, shared by every n).  A
-// wave runs one segment of 64 trials (one per lane: the segment's control
-// flow and its matrix loads are wave-uniform), so a batch's generation is
-// (batch / 64) x ceil(D / kSeg) independent waves instead of 64 sequential
-// chains of D draws.
+// into units of kUnit draws and every segment starts from J_{u kUnit} · s (a
+// host-built table, one matrix per unit index, shared by every n).  Alice's
+// cheap draws go kAliceUnits units to a segment, the shuffle's and the
+// punctured draws (a 64-bit product and a division each) one unit.  A wave
+// runs one segment of 64 trials (one per lane: the segment's control flow
+// and its matrix loads are wave-uniform), so a batch's generation is
+// (batch / 64) x segments independent waves instead of 64 sequential chains
+// of D draws.
 //
 // What each draw means is fixed by its index alone, except that a shuffle
 // draw may be rejected by _S_nd (probability < range / 2^64 per draw: < 1e-9
@@ -56,7 +58,8 @@
 namespace qldpc {
 namespace {
 
-constexpr int kSeg = 512;            // draws per segment (one wave runs one segment of 64 trials)
+constexpr int kUnit = 128;      // draws per jump-table unit (one wave runs one segment of 64 trials)
+constexpr int kAliceUnits = 4;  // units per segment in Alice's part of the stream
 constexpr uint32_t kPrefixLds = 16384;  // k-prefix entries the finish kernel keeps in LDS (a and p: 128 KiB)
 
 struct Xoshiro256pp {
@@ -103,12 +106,32 @@ __device__ inline uint64_t draw_below(Xoshiro256pp &g, uint64_t range) {
     return hi;
 }
 
-// (x / b1, x % b1) of __gen_two_uniform_ints.  For x < 2^51 the quotient
-// through f64 is exact: x and b1 are exact doubles, and when x / b1 is not an
-// integer it lies at least 1 / b1 below the next integer N + 1, more than
-// half an ulp of N + 1 < 2^52 / b1 (b1 (N + 1) <= x + b1 < 2^52) — so the
-// correctly rounded quotient truncates to floor(x / b1).
+// (x / b1, x % b1) of __gen_two_uniform_ints, x < b1 (b1 - 1).
+// b1 < 2^20 (n < 2^20 - 2): an f32 estimate — x and 1 / b1 each within 2^-23
+// relative, the product within 3e-7, so for a quotient below 2^20 the
+// truncated estimate is off by at most one — corrected by the remainder's
+// sign and size.  Otherwise, for x < 2^51 the quotient through f64 is exact:
+// x and b1 are exact doubles, and when x / b1 is not an integer it lies at
+// least 1 / b1 below the next integer N + 1, more than half an ulp of
+// N + 1 < 2^52 / b1 (b1 (N + 1) <= x + b1 < 2^52), so the correctly rounded
+// quotient truncates to floor(x / b1).  Beyond that, integer division.
 __device__ inline void split_two(uint64_t x, uint64_t b1, uint64_t &p1, uint64_t &p2) {
+    if (b1 < (1ull << 20)) {
+        const float xf = __builtin_fmaf((float)(uint32_t)(x >> 32), 4294967296.0f, (float)(uint32_t)x);
+        const float qf = xf * __builtin_amdgcn_rcpf((float)(uint32_t)b1);
+        int64_t q = (int64_t)(uint32_t)qf;
+        int64_t r = (int64_t)x - q * (int64_t)b1;
+        if (r < 0) {
+            --q;
+            r += (int64_t)b1;
+        } else if (r >= (int64_t)b1) {
+            ++q;
+            r -= (int64_t)b1;
+        }
+        p1 = (uint64_t)q;
+        p2 = (uint64_t)r;
+        return;
+    }
     if (x < (1ull << 51)) {
         p1 = (uint64_t)((double)x / (double)b1);
     } else {
@@ -118,12 +141,30 @@ __device__ inline void split_two(uint64_t x, uint64_t b1, uint64_t &p1, uint64_t
 }
 
 // One trial's draw stream: [0, n) Alice's bits, [n, n + S) the shuffle,
-// [n + S, D) the punctured draws (Alice's, Bob's per position).
+// [n + S, D) the punctured draws (Alice's, Bob's per position).  Segments:
+// units [0, ceil(n / kUnit)) in groups of kAliceUnits (the last group may
+// reach into the shuffle), then one unit each.
 struct TrialStream {
-    uint64_t n, S, D;
+    uint64_t n, S, D, units, aseg;
     __host__ __device__ TrialStream(int n_, int n_punct)
         : n((uint64_t)n_), S((n_ % 2 == 0) ? (uint64_t)n_ / 2 : (uint64_t)(n_ - 1) / 2),
-          D((uint64_t)n_ + S + 2 * (uint64_t)n_punct) {}
+          D((uint64_t)n_ + S + 2 * (uint64_t)n_punct), units((D + kUnit - 1) / kUnit),
+          aseg(((n + kUnit - 1) / kUnit + kAliceUnits - 1) / kAliceUnits) {}
+    __host__ __device__ uint64_t segments() const {
+        const uint64_t au = aseg * kAliceUnits < units ? aseg * kAliceUnits : units;
+        return aseg + (units - au);
+    }
+    // first and one-past-last unit of segment j
+    __host__ __device__ void seg_units(uint64_t j, uint64_t &u0, uint64_t &u1) const {
+        if (j < aseg) {
+            u0 = j * kAliceUnits;
+            u1 = u0 + kAliceUnits;
+        } else {
+            u0 = aseg * kAliceUnits + (j - aseg);
+            u1 = u0 + 1;
+        }
+        if (u1 > units) u1 = units;
+    }
 };
 
 // Generator workspace, uint32 words, BP = batch rounded up to 64:
@@ -152,16 +193,17 @@ __global__ void __launch_bounds__(64) trials_draw_kernel(int n, uint32_t k, int 
     const bool act = f < batch;
     const TrialStream T(n, n_punct);
     const TrialWs W(k, batch);
-    const uint64_t seg = blockIdx.x;
-    uint64_t d = seg * kSeg;
-    const uint64_t d1 = (d + kSeg < T.D) ? d + kSeg : T.D;
+    uint64_t u0, u1;
+    T.seg_units(blockIdx.x, u0, u1);
+    uint64_t d = u0 * kUnit;
+    const uint64_t d1 = (u1 * kUnit < T.D) ? u1 * kUnit : T.D;
     Xoshiro256pp g((act ? seeds[f] : 0ull) + seed_add);
-    if (seg > 0) {  // the state at draw seg * kSeg: J · s over GF(2)
+    if (u0 > 0) {  // the state at draw u0 * kUnit: J · s over GF(2)
         // the segment's matrix (8 KiB) staged in LDS by one coalesced load round
         // (eight 16-byte loads per lane in flight), then its columns read by
         // broadcast LDS reads
         __shared__ uint4 jl[512];
-        const uint4 *J4 = reinterpret_cast<const uint4 *>(jt + seg * 1024);
+        const uint4 *J4 = reinterpret_cast<const uint4 *>(jt + u0 * 1024);
         uint4 v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = J4[q * 64 + lane];
@@ -512,8 +554,8 @@ int xoshiro_jump_check(uint64_t seed, uint64_t d, uint64_t *state_out) {
 
 namespace {
 
-// Jump tables: entry j = J_{j kSeg} (column-major, 1024 words), entry 0 the
-// identity, entry j + 1 = J_kSeg · entry j by four-Russians tables of J_kSeg
+// Jump tables: entry j = J_{j kUnit} (column-major, 1024 words), entry 0 the
+// identity, entry j + 1 = J_kUnit · entry j by four-Russians tables of J_kUnit
 // (32 byte-groups x 256 column combinations).  One table per device, shared by
 // every n; it grows to the longest stream asked for and is never freed (a
 // retired shorter copy may still be read by a launch in flight).
@@ -525,7 +567,7 @@ struct JumpTable {
 std::mutex g_jt_mu;
 std::map<int, JumpTable> g_jt;
 std::vector<uint64_t> g_jt_host;  // host entries, shared by the devices
-std::vector<uint64_t> g_jl_russ;  // J_kSeg as 32 x 256 column combinations (4 words each)
+std::vector<uint64_t> g_jl_russ;  // J_kUnit as 32 x 256 column combinations (4 words each)
 
 void jt_extend_host(size_t entries) {  // (g_jt_mu held)
     if (g_jt_host.empty()) {
@@ -533,7 +575,7 @@ void jt_extend_host(size_t entries) {  // (g_jt_mu held)
         xo_jump_matrix(0, I);
         g_jt_host.assign(I, I + 1024);
         uint64_t J[1024];
-        xo_jump_matrix((uint64_t)kSeg, J);
+        xo_jump_matrix((uint64_t)kUnit, J);
         g_jl_russ.assign(32 * 256 * 4, 0);
         for (int grp = 0; grp < 32; ++grp)
             for (int b = 1; b < 256; ++b) {
@@ -547,7 +589,7 @@ void jt_extend_host(size_t entries) {  // (g_jt_mu held)
     while (g_jt_host.size() / 1024 < entries) {
         const uint64_t *B = &g_jt_host[g_jt_host.size() - 1024];
         uint64_t C[1024];
-        for (int c = 0; c < 256; ++c) {  // column c of J_kSeg · B
+        for (int c = 0; c < 256; ++c) {  // column c of J_kUnit · B
             uint64_t r[4] = {0, 0, 0, 0};
             for (int grp = 0; grp < 32; ++grp) {
                 const unsigned byte = (unsigned)(B[4 * c + grp / 8] >> (8 * (grp % 8))) & 0xffu;
@@ -598,11 +640,11 @@ hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds
     if (!scratch || n <= 0 || n_err == 0 || n_err > (uint64_t)n || n_punct < 0) return hipErrorInvalidValue;
     const TrialStream T(n, n_punct);
     const TrialWs W(n_err, batch);
-    const size_t nseg = (size_t)((T.D + kSeg - 1) / kSeg);
+    const size_t nseg = (size_t)T.segments();
     const int ngrp = (batch + 63) / 64;
     if (nseg > 0x7fffffff || ngrp > 65535) return hipErrorInvalidValue;
     const uint64_t *jt = nullptr;
-    hipError_t e = jump_table_on_device(nseg, &jt);
+    hipError_t e = jump_table_on_device((size_t)T.units, &jt);
     if (e != hipSuccess) return e;
     // last[] (0 = no writer) and the rejection flags start cleared
     if ((e = hipMemsetAsync(scratch + W.last(), 0, W.k * W.BP * sizeof(uint32_t), stream)) != hipSuccess) return e;

@@ -194,6 +194,24 @@ def test_f64_quotient_is_exact_below_2_51():
             assert int(float(x) / float(b1)) == x // b1
 
 
+def test_f32_quotient_estimate_within_one():
+    """split_two's f32 path (trials.hip, b1 < 2^20): the truncated estimate
+    fl(fl(fma(hi, 2^32, fl(lo))) * r) with r within one ulp of 1 / b1 (the
+    hardware reciprocal's bound) is within one of floor(x / b1), so one
+    remainder correction gives the exact (x / b1, x % b1)."""
+    rng = np.random.default_rng(11)
+    f32 = np.float32
+    for b1 in list(rng.integers(3, 1 << 20, 3000)) + [3, 4, 102402, (1 << 20) - 1]:
+        b1 = int(b1)
+        xs = [int(v) for v in rng.integers(0, b1 * (b1 - 1), 40, dtype=np.int64)] + [b1 * (b1 - 1) - 1, b1 - 1, 0]
+        r0 = f32(1.0) / f32(b1)
+        for r in (r0, np.nextafter(r0, f32(0)), np.nextafter(r0, f32(1))):
+            for x in xs:
+                xf = f32(float(x >> 32) * 4294967296.0 + float(f32(x & 0xFFFFFFFF)))
+                q = int(f32(xf * r))
+                assert abs(q - x // b1) <= 1, (b1, x)
+
+
 @pytest.mark.parametrize("n,qber,seed", [(1024, 0.0215, 5), (1023, 0.05, 2**63 + 11), (10240, 0.013, 1022025)])
 def test_oracle_trial_matches_python_restatement(n, qber, seed):
     a, b, q = P.trial(n, qber, seed)
