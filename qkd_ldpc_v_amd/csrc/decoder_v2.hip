@@ -1142,7 +1142,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
             };
             if constexpr (SPLIT) {  // totals in global memory: a group's four loads issued together
+#ifdef QL_DIAG_SCAN_HOT  // (diagnostic A/B only: every total read from 256 L1-hot entries — wrong decodes)
+                meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & 255)]; }, scan_slot);
+#else
                 meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
+#endif
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { scan_slot(k, mt, tot_at(mt)); });
             }

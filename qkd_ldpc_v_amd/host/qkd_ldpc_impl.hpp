@@ -208,8 +208,22 @@ class Coalescer {
                 }
             }
             lk.unlock();
-            run(g, n, m, p0, b);
+            try {
+                run(g, n, m, p0, b);
+            } catch (const std::exception &e) {  // (e.g. bad_alloc staging the batch)
+                for (Req *x : b) {
+                    x->rc = -1;
+                    x->err = e.what();
+                }
+            } catch (...) {
+                for (Req *x : b) {
+                    x->rc = -1;
+                    x->err = "unknown exception";
+                }
+            }
             lk.lock();
+            // every caller of the batch is released and the next leader may
+            // start, whatever run() did
             for (Req *x : b) x->done = true;
             busy_ = false;
             cv_.notify_all();
@@ -280,20 +294,33 @@ struct GraphEntry {
 // (HKey, one pass over the adjacency, computed without any lock), so an H
 // freed and another allocated at the same address, or an H reloaded in place
 // (the reference's config-after-config loop), never picks up a stale graph.
-// An in-place edit that leaves all 128 sampled lists unchanged is not seen by
-// the fast key: call release() after one.  DESIGN.md §2 has the costs.
+// An in-place edit that leaves all 128 sampled lists unchanged is seen by the
+// fast key only at an entry's next full check (every kVerifyEvery-th hit):
+// call release() after one to drop the graph at once.  DESIGN.md §2 has the
+// costs.
 class GraphCache {
   public:
     template <class Matrix>
     std::shared_ptr<GraphEntry> get(const Matrix &H) {
         const HFastKey fk = fast_key_of(H);
         {
-            std::lock_guard<std::mutex> lk(mu_);
-            for (auto it = lru_.begin(); it != lru_.end(); ++it)
-                if (it->fast == fk) {
-                    lru_.splice(lru_.begin(), lru_, it);
-                    return lru_.front().e;
-                }
+            std::shared_ptr<GraphEntry> hit;
+            HKey hk;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                for (auto it = lru_.begin(); it != lru_.end(); ++it)
+                    if (it->fast == fk) {
+                        lru_.splice(lru_.begin(), lru_, it);
+                        // every kVerifyEvery-th hit of an entry re-checks the whole
+                        // content, so an in-place edit the sampled lists miss is
+                        // caught within that many calls (release() at once)
+                        if (++it->hits % kVerifyEvery != 0) return lru_.front().e;
+                        hit = it->e;
+                        hk = it->key;
+                        break;
+                    }
+            }
+            if (hit && key_of(H) == hk) return hit;
         }
         const HKey k = key_of(H);
         {
@@ -322,7 +349,7 @@ class GraphCache {
                 lru_.splice(lru_.begin(), lru_, it);
                 return lru_.front().e;
             }
-        lru_.push_front(Slot{k, fk, e});
+        lru_.push_front(Slot{k, fk, e, 0});
         while (lru_.size() > capacity_) lru_.pop_back();  // callers still holding it keep it alive
         return e;
     }
@@ -362,7 +389,9 @@ class GraphCache {
         HKey key;
         HFastKey fast;
         std::shared_ptr<GraphEntry> e;
+        uint64_t hits = 0;
     };
+    static constexpr uint64_t kVerifyEvery = 32;
     std::mutex mu_;
     std::list<Slot> lru_;
     size_t capacity_ = 4;

@@ -24,7 +24,12 @@
 //       the reference's config-after-config loop: trials on A, then B loaded
 //       INTO THE SAME H_matrix object (same address, same n/m/nnz when B is a
 //       column permutation of A), trials on B: "A ..." / "B ..." lines.
+//   run_trial_check inplace <matrix> <format>
+//       the graph cache after an in-place edit its O(1) key cannot see (two
+//       unsampled rows swap their check ids): "inplace fastkey_same 1
+//       detected_after <calls>" — the periodic full check's catch.
 // Failures print "ERROR: <what>" and exit 1, like the reference's main.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -148,7 +153,44 @@ int main(int argc, char **argv) {
             for (unsigned long long seed : seeds) print("B ", run_trial(H, qber, (size_t)seed, {}, sf));
             return 0;
         }
-        std::fprintf(stderr, "usage: run_trial_check load|trials|reuse ... (see the file header)\n");
+        if (mode == "inplace" && argc >= 4) {
+            // an in-place edit of H that the O(1) fast key cannot see: two rows
+            // and the bits they hold, none of them among the 128 sampled lists,
+            // swap their check ids; the cache must pick up the new content by
+            // its periodic full check
+            H_matrix H;
+            load_into(H, argv[2], std::atoi(argv[3]));
+            namespace qi = qkd_ldpc_v_amd::impl;
+            auto &cache = qi::graph_cache();
+            const auto e0 = cache.get(H);
+            const size_t m = H.check_nodes.size(), n = H.bit_nodes.size();
+            const size_t rs = m > 64 ? m / 64 : 1, cs = n > 64 ? n / 64 : 1;
+            auto free_row = [&](size_t j) {
+                if (j % rs == 0) return false;
+                for (int b : H.check_nodes[j])
+                    if ((size_t)b % cs == 0) return false;
+                return true;
+            };
+            size_t j1 = m, j2 = m;
+            for (size_t j = 0; j < m && j2 == m; ++j)
+                if (free_row(j)) (j1 == m ? j1 : j2) = j;
+            if (j2 == m) throw std::runtime_error("no pair of unsampled rows");
+            const auto fk0 = qi::fast_key_of(H);
+            std::swap(H.check_nodes[j1], H.check_nodes[j2]);  // (swaps the buffers: unsampled rows)
+            for (size_t j : {j1, j2})
+                for (int b : H.check_nodes[j]) {
+                    auto &col = H.bit_nodes[b];
+                    for (int &x : col) x = (x == (int)j1) ? (int)j2 : (x == (int)j2) ? (int)j1 : x;
+                    std::sort(col.begin(), col.end());
+                }
+            const bool same = qi::fast_key_of(H) == fk0;
+            int detected = -1;
+            for (int c = 1; c <= 64 && detected < 0; ++c)
+                if (cache.get(H) != e0) detected = c;
+            std::printf("inplace fastkey_same %d detected_after %d\n", same ? 1 : 0, detected);
+            return 0;
+        }
+        std::fprintf(stderr, "usage: run_trial_check load|trials|reuse|inplace ... (see the file header)\n");
         return 2;
     } catch (const std::exception &e) {
         std::printf("ERROR: %s\n", e.what());

@@ -148,6 +148,17 @@ def test_graph_cache_same_address_new_edges(gpu_available, tmp_path):
     assert parse(lines, "B ") == oracle_trials(HB, Q.SPA, 0.0, 0.0, 0.03, 50, seeds)
 
 
+@pytest.mark.gpu
+def test_graph_cache_catches_unsampled_inplace_edit(gpu_available, tmp_path):
+    """An in-place edit of H that leaves the O(1) fast key unchanged (two
+    unsampled rows swap their check ids) is caught by the cache's periodic
+    full-content check (every 32nd hit of an entry): a new device graph."""
+    lines = run(["inplace", matrix_path("c2_n10240_m2201.alist"), 1], tmp_path)
+    f = [ln for ln in lines if ln.startswith("inplace")][0].split()
+    assert f[2] == "1", lines
+    assert 1 <= int(f[4]) <= 32, lines
+
+
 def test_dropin_refuses_non_bit_syndrome():
     """The reference's decoders read syndrome[j] as a sign (any non-zero: -1,
     src/qkd_ldpc_algorithm.cpp:57) and compare it by value (:101); the kernels
