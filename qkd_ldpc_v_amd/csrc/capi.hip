@@ -205,6 +205,7 @@ struct qldpc_graph {
     long long stage_doubles = 0;            // V2 hybrid: staged VN terms per frame
     int split_k = 1, split_mrows = 0;       // V2 split: workgroups per frame, rows of the largest part
     int split_cb = 0, split_nc = 0;         // V2 split exchange gather: bits per LDS chunk, chunks per part (0: off)
+    int split_pl = REG_TSTRIDE;             // V2 split: a part's lanes (1024: 16 waves; 512: 8 waves, 2 per CU)
     bool kernel_timing = false;             // qldpc_set_kernel_timing
     std::vector<int32_t> col_lab;           // V2 bank relabelling (relabel.cpp): bit id -> label; empty: identity
     long long relabel_stats[4] = {0, 0, 0, 0};  // bank excess before / after, busiest-bank cycles before / after
@@ -225,12 +226,12 @@ const char *variant_name(int v) {
 
 // Threads per workgroup: the graph's lanes, or one part's for split frames.
 int block_threads(const qldpc_graph &g) {
-    return (g.variant == VAR_V2 && g.split_k > 1) ? REG_TSTRIDE : g.T;
+    return (g.variant == VAR_V2 && g.split_k > 1) ? g.split_pl : g.T;
 }
 
 size_t lds_of(const qldpc_graph &g, int alg) {
     if (g.variant == VAR_V2 && g.split_k > 1)
-        return lds_bytes_v2(alg, g.n, g.split_mrows, 1024, true, 0, 0, -1, g.split_cb);
+        return lds_bytes_v2(alg, g.n, g.split_mrows, g.split_pl, true, 0, 0, -1, g.split_cb);
     return g.variant == VAR_V2 ? lds_bytes_v2(alg, g.n, g.m, g.T, false, g.v2R, g.v2RG,
                                               (g.rows_global_ms && alg >= 2) ? g.rows_lds_ms : -1)
                                : lds_bytes_for(g.variant, g.n, g.m, g.T);
@@ -471,28 +472,41 @@ bool plan_v2(qldpc_graph &g, const int32_t *row_ptr) {
 }
 
 // V2 split plan, for codes whose frame does not fit one CU (totals beyond LDS
-// or more edges than 16 waves x 64 lanes x 40 slots): K parts of 16 waves
-// each (one workgroup per part, K <= 16 so a part group fits well inside one
-// XCD's 32 CUs), rows dealt to the 16K waves as in plan_v2 (contiguous
-// balanced blocks), part r = waves [16r, 16r + 16).  Totals go to global
-// memory.  QLDPC_SPLIT=0 disables it (v1 is used).
+// or more edges than 16 waves x 64 lanes x 40 slots): K parts of WR waves
+// each (one workgroup per part), rows dealt to the WR K waves as in plan_v2
+// (contiguous balanced blocks).  Totals go to global memory.  Parts are 16
+// waves (one per CU), or 8 waves (two per CU, half the LDS each) when that
+// lets more frames run at once on an XCD's 32 CUs: a frame's time per
+// iteration is set by latency, not by its part count (C4 (ii), n = 102400,
+// dv = 4: K = 11, 12 and 16 parts of 16 waves decode in the same 24.0-24.1 ms,
+// two frames per XCD each — 32 = 2 x 11 + 10 leaves 10 CUs waiting; with
+// 8-wave parts K = 21 runs three per XCD).  The graph's per-part arrays keep
+// a stride of 16 waves / REG_TSTRIDE lanes either way (8-wave parts leave
+// waves 8..15 of each part empty), so part r = waves [16r, 16r + 16).
+// QLDPC_SPLIT=0 disables it (v1 is used); QLDPC_SPLIT_K / QLDPC_SPLIT_WP force
+// the part count / size.
 bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_idx) {
     if (env_int("QLDPC_SPLIT", 1) == 0) return false;
     if (g.max_dc <= 0 || g.max_dc > 32 || g.n + 1 > (int)META_COL_MASK) return false;
     for (int j = 0; j < g.m; ++j)
         if (row_ptr[j + 1] == row_ptr[j]) return false;
     const long long E = g.E;
-    const int WP = REG_TSTRIDE / 64;
-    // One attempt: K parts of R slots per lane.
-    auto attempt = [&](int K, int R) -> bool {
-        const int W = WP * K;
-        const long long cap = 64LL * std::max<long long>((E + 64LL * W - 1) / (64LL * W), g.max_dc);
+    const int WP = REG_TSTRIDE / 64;  // waves per part in the graph's arrays
+    // One attempt: K parts of WR waves, R slots per lane.
+    auto attempt = [&](int K, int R, int WR) -> bool {
+        const int PL = WR * 64;                                  // the part's lanes (threads)
+        const size_t LIM = (size_t)LDS_LIMIT * WR / WP;           // its LDS: 1 or 2 parts per CU
+        const int W = WP * K, Wr = WR * K;
+        const long long cap = 64LL * std::max<long long>((E + 64LL * Wr - 1) / (64LL * Wr), g.max_dc);
         if (cap > 64LL * R) return false;
         std::vector<long long> sums;
-        const auto waves = balance_rows(row_ptr, g.m, W, cap, sums);
+        const auto waves = balance_rows(row_ptr, g.m, Wr, cap, sums);
         std::vector<int> order, rb(W + 1, 0), nrp(g.m + 1, 0);
-        for (int w = 0; w < W; ++w) {
-            order.insert(order.end(), waves[w].begin(), waves[w].end());
+        for (int w = 0; w < W; ++w) {  // wave w = part w / WP, its (w % WP)-th wave (empty past WR)
+            if (w % WP < WR) {
+                const auto &wr = waves[(w / WP) * WR + w % WP];
+                order.insert(order.end(), wr.begin(), wr.end());
+            }
             rb[w + 1] = (int)order.size();
         }
         if ((int)order.size() != g.m) return false;
@@ -518,8 +532,8 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         int mrows = 0;
         for (int r = 0; r <= K; ++r) prow[r] = rb[std::min(W, r * WP)];
         for (int r = 0; r < K; ++r) mrows = std::max(mrows, prow[r + 1] - prow[r]);
-        if (lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, 0) > LDS_LIMIT ||
-            lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, 0) > LDS_LIMIT)
+        if (lds_bytes_v2(2, g.n, mrows, PL, true, 0, 0, -1, 0) > LIM ||
+            lds_bytes_v2(0, g.n, mrows, PL, true, 0, 0, -1, 0) > LIM)
             return false;
         // Exchange gather (DecodeArgs::xoff): the largest LDS chunk of a part's
         // bits every algorithm's layout holds (SPA keeps its LDS message slots
@@ -528,11 +542,11 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         int cb = 0, nc = 0;
         if (env_int("QLDPC_SPLIT_X", 1)) {
             const int own = (g.n + K - 1) / K;
-            const bool rl0 = v2_split_rl_fits(g.n, mrows, 0);
+            const bool rl0 = v2_split_rl_fits(g.n, mrows, 0, PL);
             auto fits = [&](int c) {
-                return lds_bytes_v2(2, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, c) <= LDS_LIMIT &&
-                       lds_bytes_v2(0, g.n, mrows, REG_TSTRIDE, true, 0, 0, -1, c) <= LDS_LIMIT &&
-                       (!rl0 || v2_split_rl_fits(g.n, mrows, c));
+                return lds_bytes_v2(2, g.n, mrows, PL, true, 0, 0, -1, c) <= LIM &&
+                       lds_bytes_v2(0, g.n, mrows, PL, true, 0, 0, -1, c) <= LIM &&
+                       (!rl0 || v2_split_rl_fits(g.n, mrows, c, PL));
             };
             int lo = 0, hi = std::min(own, 0xFFFF);
             while (lo < hi) {
@@ -558,18 +572,31 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         g.part_row0 = prow;
         g.split_cb = cb;
         g.split_nc = nc;
+        g.split_pl = PL;
         return true;
     };
-    // QLDPC_SPLIT_K forces the part count (<= 32: one XCD's CUs)
-    const long long cap_part = (long long)WP * 64 * V2_R_TIGHT;
-    const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
+    // The smallest feasible K for each part size, then the size that runs more
+    // frames per XCD at once (32 CUs: 32 parts of 16 waves or 64 of 8; ties:
+    // 16 waves, fewer group members).  (K need not divide an XCD's parts:
+    // groups form in claim order and a workgroup joins the next group whenever
+    // it finishes a frame.)
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
-    if (kforce && (kforce < kmin || kforce > 32)) return false;
-    // (K need not divide an XCD's 32 workgroups: groups form in claim order and
-    // a workgroup joins the next group whenever it finishes a frame)
-    for (int K = kforce ? kforce : kmin; K <= (kforce ? kforce : 16); ++K)
-        if (attempt(K, V2_R_TIGHT)) return true;
-    return false;
+    const int wforce = env_int("QLDPC_SPLIT_WP", 0);
+    if (wforce && wforce != 16 && wforce != 8) return false;
+    auto smallest_k = [&](int WR) -> int {
+        const long long cap_part = (long long)WR * 64 * V2_R_TIGHT;
+        const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
+        if (kforce) return (kforce >= kmin && kforce <= 32 && attempt(kforce, V2_R_TIGHT, WR)) ? kforce : 0;
+        for (int K = kmin; K <= 32; ++K)
+            if (attempt(K, V2_R_TIGHT, WR)) return K;
+        return 0;
+    };
+    const int k16 = (wforce == 8) ? 0 : smallest_k(16);
+    const int k8 = (wforce == 16) ? 0 : smallest_k(8);
+    const int f16 = k16 ? 32 / k16 : 0, f8 = k8 ? 64 / k8 : 0;
+    if (!k16 && !k8) return false;
+    if (k8 && (f8 > f16 || !k16)) return attempt(k8, V2_R_TIGHT, 8);  // (the last attempt sets the plan)
+    return attempt(k16, V2_R_TIGHT, 16);
 }
 
 template <typename T>
@@ -1763,7 +1790,8 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
     // (a host-only graph answers everything but the device's workgroup count)
     if (!dg && !(g->devs.empty() && !workgroups)) return fail(QLDPC_EINVAL, "graph does not live on that device");
     const size_t lds = lds_of(*g, algorithm);
-    if (lanes) *lanes = g->T;
+    // (split frames: the lanes that run — K parts of split_pl — not the arrays' stride)
+    if (lanes) *lanes = (g->variant == VAR_V2 && g->split_k > 1) ? g->split_k * g->split_pl : g->T;
     if (edges_per_lane) *edges_per_lane = g->EPL;
     if (lds_bytes) *lds_bytes = (int32_t)lds;
     if (variant)

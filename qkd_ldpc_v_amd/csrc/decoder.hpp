@@ -208,7 +208,7 @@ size_t lds_bytes_v2(int alg, int n, int m, int T, bool split = false, int R = 0,
 // positions' two code bits fit the LDS byte area.
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m);
 // Split frames: whether the SPA layout keeps its LDS message slots at gcb exchange-gather bits.
-bool v2_split_rl_fits(int n, int mrows, int gcb);
+bool v2_split_rl_fits(int n, int mrows, int gcb, int pl);
 constexpr int V2_VNG_DUMMY_CHUNKS = 64;  // hybrid: one scratch code byte per lane for dummy slots
 hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_bytes, hipStream_t stream);
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu);

@@ -132,14 +132,14 @@ struct EdgeMsgs<0> {  // per-workgroup global scratch, slot-major [k][lane]: coa
 };
 
 // V2 message storage: slots k < R - RL in VGPRs, slots R - RL <= k < R in
-// LDS, slot-major [k - (R - RL)][lane] (lane stride REG_TSTRIDE: conflict-free
-// 8-byte rows, constant offsets from one base register), and slots
+// LDS, slot-major [k - (R - RL)][lane] (lane stride LS, the workgroup's lanes:
+// conflict-free 8-byte rows, constant offsets from one base register), and slots
 // R <= k < R + RG in this workgroup's global scratch, slot-major [k - R][lane]
 // — coalesced, constant offsets, L2/MALL-resident.  A lane only ever reads
 // back what it wrote itself, so program order suffices.  The LDS slots keep
 // the register kernel within 128 VGPRs without compiler spills (scratch
 // stores whose reloads wait on the vector-memory counter).
-template <int R, int RG, int RL = 0>
+template <int R, int RG, int RL = 0, int LS = REG_TSTRIDE>
 struct EdgeMsgsH {
     static constexpr int RV = R - RL;
     double v[RV];
@@ -157,7 +157,7 @@ struct EdgeMsgsH {
     }
     __device__ __forceinline__ double get(int k) const {
         if (k < RV) return v[k];
-        if (k < R) return lp[(k - RV) * REG_TSTRIDE];
+        if (k < R) return lp[(k - RV) * LS];
         return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, (k - R) * REG_TSTRIDE * 8, 0));
     }
     // For passes that visit every slot in order (the check-node scan, the
@@ -184,7 +184,7 @@ struct EdgeMsgsH {
         if (k < RV) {
             v[k] = x;
         } else if (k < R) {
-            lp[(k - RV) * REG_TSTRIDE] = x;
+            lp[(k - RV) * LS] = x;
         } else {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), rs, voff, (k - R) * REG_TSTRIDE * 8,

@@ -72,8 +72,10 @@ constexpr int V2_A0_ENTRIES = 64;
 // holds the palette and this part's rows (m = the largest part's row count).
 struct V2Layout {
     size_t total, rows, rowflag, tail, tailneg, a0tab, ctab, msl, codes, palette, syn, bytes;
+    // ls: the lane stride of the LDS message slots (the workgroup's lanes;
+    // split parts of 8 waves use 512)
     __host__ __device__ V2Layout(int n, int m, int, int T, bool minsum, bool split = false, int rl = 0,
-                                 bool rowscan = false, int gcb = 0) {
+                                 bool rowscan = false, int gcb = 0, int ls = REG_TSTRIDE) {
         palette = V2_PAL_OFF;
         codes = split ? 0 : V2_CODES_OFF;
         size_t o = split ? V2_CODES_OFF : V2_TOTAL_OFF;
@@ -87,7 +89,7 @@ struct V2Layout {
         // the iteration-0 table, both dead between the message pass and the scan
         if (split && gcb > 0 && al16(rows + (size_t)gcb * 8) > o) o = al16(rows + (size_t)gcb * 8);
         ctab = o; o = al16(o + (minsum ? 0 : (size_t)ql_exact::EXPM1_CLASSES * (sizeof(ql_exact::Expm1A) + sizeof(ql_exact::Expm1B))));  // SPA: tanh's expm1 classes
-        msl = o; o = al16(o + (size_t)rl * REG_TSTRIDE * 8);  // message slots held in LDS
+        msl = o; o = al16(o + (size_t)rl * ls * 8);  // message slots held in LDS
         // one workgroup per frame: the rows' target syndrome bits as sign words
         // (s << 31), in the palette-index area past the codes when it has room
         syn = 0;
@@ -139,10 +141,10 @@ __device__ __forceinline__ void st_row16(__amdgpu_buffer_rsrc_t rs, int r, doubl
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, r * 16, 0, 0);
 }
 
-template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN, int R>
+template <bool SPLIT, int RL, bool RGLB, bool ROWSCAN, int R, int PL>
 __device__ __forceinline__ V2Layout v2_layout(const DecodeArgs &a, bool minsum) {
     if constexpr (SPLIT)
-        return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL, false, a.split_cb);
+        return V2Layout(a.n, a.split_mrows, a.nc, a.T, minsum, true, RL, false, a.split_cb, PL);
     else return V2Layout(a.n, RGLB ? a.rows_lds : a.m, a.nc, a.T, minsum, false, RL, ROWSCAN);
 }
 
@@ -160,9 +162,11 @@ __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, in
 #define QL_RL_SPLIT 12
 #endif
 constexpr int V2_RL_SPLIT = QL_RL_SPLIT;
-__host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows, int gcb) {
-    return alg <= 1 &&
-           V2Layout(n, mrows, (n + 3) / 4, REG_TSTRIDE, false, true, V2_RL_SPLIT, false, gcb).bytes <= 160 * 1024;
+// pl: the part's lanes (1024, or 512 for parts of 8 waves, two per CU: half
+// the LDS each).
+__host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows, int gcb, int pl = REG_TSTRIDE) {
+    return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, pl, false, true, V2_RL_SPLIT, false, gcb, pl).bytes <=
+                           (size_t)160 * 1024 * pl / REG_TSTRIDE;
 }
 
 constexpr int V2_SPLIT_SPIN_LIMIT = 1 << 22;  // ~seconds of polling: a broken group ends, never hangs
@@ -209,7 +213,11 @@ __device__ __forceinline__ lds_f64 *col_off8(uint32_t mt, uint32_t base) {
     return (lds_f64 *)(uintptr_t)o;
 }
 
-template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false, bool RGLB = false>
+// PL (split frames): the part's lanes — 1024 (16 waves, one part per CU) or
+// 512 (8 waves, two parts per CU; the register budget stays that of 1024
+// threads).  The graph's per-part arrays keep a stride of REG_TSTRIDE lanes /
+// 16 waves either way (planner: parts of 8 waves leave waves 8..15 empty).
+template <int ALG, int R, int RG, bool SPLIT, int RL = 0, bool VNG = false, bool RGLB = false, int PL = REG_TSTRIDE>
 __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool SPA_FAM = (ALG == 0 || ALG == 1);
@@ -240,7 +248,8 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
     const double thr = a.thr_on ? a.thr : __builtin_inf();
     const double lim = thr < 44.0 ? thr : 44.0;  // SPA: tanh(+-b/2) = +-1 for |b| >= 44, clipped or not
     static_assert(!RGLB || (VNG && RG > 0), "rows in global scratch: hybrid bit gather only");
-    const V2Layout L = v2_layout<SPLIT, RL, RGLB, ROWSCAN, R>(a, !SPA_FAM);
+    static_assert(PL == REG_TSTRIDE || SPLIT, "half-size parts: split frames only");
+    const V2Layout L = v2_layout<SPLIT, RL, RGLB, ROWSCAN, R, PL>(a, !SPA_FAM);
     int *s_frame = reinterpret_cast<int *>(smem);
     int *s_flag = reinterpret_cast<int *>(smem) + 1;
     int *s_part = reinterpret_cast<int *>(smem) + 2;  // SPLIT: rank, sync slot
@@ -287,7 +296,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         else return total[(int)(mt & META_COL_MASK)];
     };
 
-    EdgeMsgsH<R, RG, RL> c2b;
+    EdgeMsgsH<R, RG, RL, PL> c2b;
     c2b.bind(a.scratch + (size_t)blockIdx.x * a.scratch_wg_doubles, tid);
     c2b.bind_lds(reinterpret_cast<double *>(smem + L.msl), tid);
     MetaSrcW<S> meta;
@@ -1402,15 +1411,15 @@ __global__ void __launch_bounds__(256) palettize_kernel(int n, int nc, const dou
 
 using KernelFn = void (*)(DecodeArgs);
 
-template <int R, int RG, bool SPLIT = false>
+template <int R, int RG, bool SPLIT = false, int PL = REG_TSTRIDE>
 KernelFn pick_v2(int alg) {
     switch (alg) {
-    case 0: return decode_v2_kernel<0, R, RG, SPLIT>;
-    case 1: return decode_v2_kernel<1, R, RG, SPLIT>;
-    case 2: return decode_v2_kernel<2, R, RG, SPLIT>;
-    case 3: return decode_v2_kernel<3, R, RG, SPLIT>;
-    case 4: return decode_v2_kernel<4, R, RG, SPLIT>;
-    default: return decode_v2_kernel<5, R, RG, SPLIT>;
+    case 0: return decode_v2_kernel<0, R, RG, SPLIT, 0, false, false, PL>;
+    case 1: return decode_v2_kernel<1, R, RG, SPLIT, 0, false, false, PL>;
+    case 2: return decode_v2_kernel<2, R, RG, SPLIT, 0, false, false, PL>;
+    case 3: return decode_v2_kernel<3, R, RG, SPLIT, 0, false, false, PL>;
+    case 4: return decode_v2_kernel<4, R, RG, SPLIT, 0, false, false, PL>;
+    default: return decode_v2_kernel<5, R, RG, SPLIT, 0, false, false, PL>;
     }
 }
 
@@ -1439,7 +1448,13 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
     }
 }
 
-KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
+KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl, int pl = REG_TSTRIDE) {
+    if (split_k > 1 && pl == REG_TSTRIDE / 2) {
+        constexpr int H = REG_TSTRIDE / 2;
+        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT, false, false, H>
+                                : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT, false, false, H>;
+        return pick_v2<V2_R_TIGHT, 0, true, H>(alg);
+    }
     if (split_k > 1) {
         if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT>
                                 : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT>;
@@ -1455,16 +1470,16 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl) {
 }  // namespace
 
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds, int gcb) {
-    if (split)
-        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb) ? V2_RL_SPLIT : 0,
-                        false, gcb)
+    if (split)  // (T: the part's lanes)
+        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb, T) ? V2_RL_SPLIT : 0,
+                        false, gcb, T)
             .bytes;
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
     return V2Layout(n, rows_lds >= 0 ? rows_lds : m, (n + 3) / 4, T, alg >= 2, split, rl ? V2_RL : 0,
                     V2_ROWSCAN_ON && !split && RG == 0).bytes;
 }
 
-bool v2_split_rl_fits(int n, int mrows, int gcb) { return v2_use_rl_split(0, n, mrows, gcb); }
+bool v2_split_rl_fits(int n, int mrows, int gcb, int pl) { return v2_use_rl_split(0, n, mrows, gcb, pl); }
 
 bool v2_vng_ok(int alg, int R, int RG, int split_k, int dv_max, int m) {
     if (alg < 2 || split_k > 1 || m >= 0xFFFF) return false;
@@ -1487,8 +1502,10 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
     if (a.rows_wg_offset >= 0 && !(a.vn_rows && a.v2RG > 0)) return hipErrorInvalidValue;
     KernelFn k = a.vn_rows ? kernel_v2_vng(a.alg, a.v2RG, a.rows_wg_offset >= 0)
                            : kernel_v2(a.v2R, a.v2RG, a.split_k, a.alg,
-                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb)
-                                                     : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T));
+                                       a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb, a.T)
+                                                     : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T),
+                                       a.split_k > 1 ? a.T : REG_TSTRIDE);
+    if (a.split_k > 1 && a.T != REG_TSTRIDE && a.T != REG_TSTRIDE / 2) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;
@@ -1497,7 +1514,7 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 }
 
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
-    KernelFn k = kernel_v2(R, RG, split_k, alg, false);
+    KernelFn k = kernel_v2(R, RG, split_k, alg, false, split_k > 1 ? T : REG_TSTRIDE);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     if (e != hipSuccess) return e;

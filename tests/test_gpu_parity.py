@@ -321,19 +321,50 @@ def test_c4_100k_split_full_decode(gpu_available):
     assert out.iterations.min() < 50
 
 
+@pytest.mark.parametrize("wp", [0, 16])
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
-def test_c4_generated_dv4_ten_parts(gpu_available, alg, prim, sec):
-    """the generated n=102400 dv=4 code needs more than
-    8 parts per frame (409,600 edges; the planner picks 11), a count that does
-    not divide an XCD's 32 workgroups."""
+def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec, wp):
+    """the generated n=102400 dv=4 code (409,600
+    edges) needs more than 8 parts of 16 waves; 11 of them leave 10 of an XCD's
+    32 CUs waiting, so the planner takes 8-wave parts, two per CU (21 parts,
+    three frames per XCD).  wp = 16 forces the 16-wave parts (K = 11), a count
+    that does not divide an XCD's 32 workgroups."""
     H = Q.regular_code(102400, 22001, 4, 777)
+    if wp:
+        monkeypatch.setenv("QLDPC_SPLIT_WP", str(wp))
     g = Q.Graph(H)
+    monkeypatch.delenv("QLDPC_SPLIT_WP", raising=False)
     plan = g.plan(0, alg)
-    assert plan["variant"] == "v2_split" and plan["lanes"] >= 10 * 1024 and plan["lanes"] % 1024 == 0, plan
+    part = 1024 if wp == 16 else 512
+    assert plan["variant"] == "v2_split" and plan["lanes"] >= 10 * 1024 and plan["lanes"] % part == 0, plan
+    if not wp:
+        assert plan["workgroups"] == 2 * 256, plan  # two 8-wave parts per CU
     O = Oracle(H)
     _, _, llr, synd = frames(H, 0.022, 6, 4242)
     out = g.decode(Q.Params(alg, 50, True, 100.0, prim, sec), llr, synd, posterior=True)
     ob, oi, ok, op = O.decode_batch(O.params(alg, 50, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
+    for f in range(llr.shape[0]):
+        assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
+        assert bits_equal_nan(out.posterior[f], op[f])
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+def test_c4_100k_split_half_parts(gpu_available, monkeypatch, alg, prim, sec):
+    """QLDPC_SPLIT_WP=8 (read when the graph is created): the C4 stand-in in
+    8-wave parts, two per CU (decoder_v2.hip PL = 512: LDS message slots at a
+    512-lane stride, the graph's per-part arrays at the 1024-lane stride with
+    waves 8..15 empty) — bit-exact with the oracle, posteriors included."""
+    H = load_fixture("c4s_n102400_m32001.alist")
+    monkeypatch.setenv("QLDPC_SPLIT_WP", "8")
+    g = Q.Graph(H)
+    monkeypatch.delenv("QLDPC_SPLIT_WP")
+    plan = g.plan(0, alg)
+    assert plan["lanes"] % 512 == 0 and plan["lanes"] >= 15 * 512, plan
+    assert plan["workgroups"] == 2 * 256, plan
+    _, _, llr, synd = frames(H, 0.038, 8, 170 + alg)
+    out = g.decode(Q.Params(alg, 12, True, 100.0, prim, sec), llr, synd, posterior=True)
+    O = Oracle(H)
+    ob, oi, ok, op = O.decode_batch(O.params(alg, 12, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
     for f in range(llr.shape[0]):
         assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
         assert bits_equal_nan(out.posterior[f], op[f])
