@@ -296,9 +296,7 @@ struct MetaSrcW : MetaSrc<R> {
         auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
 #pragma unroll
         for (int g = 0; g < R / 4; ++g) {
-#ifndef QL_TV_NOPRIO
             rotate_prio(g);
-#endif
             if (4 * g < epl_s) {
                 double tv[4];
 #pragma unroll
@@ -315,39 +313,6 @@ struct MetaSrcW : MetaSrc<R> {
             }
         }
     }
-#ifdef QL_TV_HALF
-    // (A/B) each_upto_tv with the next group's totals requested half a group
-    // early: after the group's first two slots, once its metadata (requested
-    // at the group's start) has arrived.
-    template <typename LD, typename F>
-    __device__ __forceinline__ void each_upto_tv_half(int epl_s, LD &&ld, F &&f) const {
-        asm volatile("" : "+s"(epl_s));
-        auto q = __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff, 0, 0);
-        double tv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) tv[i] = ld((uint32_t)q[i]);
-#pragma unroll
-        for (int g = 0; g < R / 4; ++g) {
-            rotate_prio(g);
-            if (4 * g < epl_s) {
-                const bool more = g + 1 < R / 4 && 4 * (g + 1) < epl_s;
-                const auto qn = more ? __builtin_amdgcn_raw_buffer_load_b128(this->rs, this->voff,
-                                                                             (g + 1) * REG_TSTRIDE * 16, 0)
-                                     : q;
-                f(4 * g + 0, (uint32_t)q[0], tv[0]);
-                if (4 * g + 1 < epl_s) f(4 * g + 1, (uint32_t)q[1], tv[1]);
-                double tn[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tn[i] = more ? ld((uint32_t)qn[i]) : 0.0;
-                if (4 * g + 2 < epl_s) f(4 * g + 2, (uint32_t)q[2], tv[2]);
-                if (4 * g + 3 < epl_s) f(4 * g + 3, (uint32_t)q[3], tv[3]);
-                q = qn;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) tv[i] = tn[i];
-            }
-        }
-    }
-#endif
     // Same as each_upto, also handing over the word of a second metadata array
     // of identical layout (rs2).
     template <typename F>

@@ -1153,8 +1153,6 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             if constexpr (SPLIT) {  // totals in global memory: a group's four loads issued together
 #ifdef QL_DIAG_SCAN_HOT  // (diagnostic A/B only: every total read from 256 L1-hot entries — wrong decodes)
                 meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & 255)]; }, scan_slot);
-#elif defined(QL_TV_HALF)
-                meta.each_upto_tv_half(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
 #else
                 meta.each_upto_tv(epl, [&](uint32_t mt) { return total[(int)(mt & META_COL_MASK)]; }, scan_slot);
 #endif
