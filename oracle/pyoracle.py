@@ -16,6 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqkdldpc_oracle.so")
 if os.environ.get("QLDPC_ASAN") == "1":  # `make asan`: the oracle under ASan + UBSan (build/asan/)
     LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "asan", "libqkdldpc_oracle.so")
+if os.environ.get("QLO_LIB_PATH"):  # tools/oracle_speed.py's timing-split build
+    LIB_PATH = os.environ["QLO_LIB_PATH"]
 
 
 class _Params(ctypes.Structure):
