@@ -31,6 +31,11 @@ constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
 #define QL_VN_BATCH 2
 #endif
 constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS round trip
+#ifndef QL_SPLIT_DEFER
+// split frames: the exit test after the message pass (1: a workgroup barrier
+// between scan and message pass, 2: a wave-local fence; 0: the test first)
+#define QL_SPLIT_DEFER 1
+#endif
 #ifndef QL_MSG_PF
 #define QL_MSG_PF 1  // stage-writing message passes request the next group's metadata early
 #endif
@@ -431,6 +436,19 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             __syncthreads();                                                 \
         }                                                                    \
     } while (0)
+        // split frames between a wave's scan and its own message pass
+#define split_local_sync()                                                   \
+    do {                                                                     \
+        if constexpr (SPLIT && QL_SPLIT_DEFER == 2) {                        \
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");           \
+            __builtin_amdgcn_wave_barrier();                                 \
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");           \
+        } else if constexpr (SPLIT && QL_SPLIT_DEFER) {                      \
+            __syncthreads();                                                 \
+        } else {                                                             \
+            psync();                                                         \
+        }                                                                    \
+    } while (0)
         const int bit_lo = SPLIT ? (int)((long long)n * rank / a.split_k) : 0;
         const int bit_hi = SPLIT ? (int)((long long)n * (rank + 1) / a.split_k) : n;
         const uint8_t *sy = a.synd + (size_t)f * m;
@@ -614,10 +632,16 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             }
         };
         // VN phases 1 .. k0-1 and the staged terms (shared by iteration 0's fast path).
-        auto vn_phases = [&]() {
+        // xchk: split frames' deferred exit test (iteration xchk - 1 ends the
+        // decode when no part flagged a mismatch), read past the first
+        // barrier; returns true to end it there, before the gather.
+        auto vn_phases = [&](int xchk) -> bool {
             STAMP(ST_CN3);
             psync();
             STAMP(ST_VN0_WAIT);
+            if constexpr (SPLIT) {
+                if (xchk && __hip_atomic_load(gmis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != xchk) return true;
+            }
             // ---- remaining VN phases: the k-th message of every bit, in check order ----
             for (int kk = 1; kk < k0; ++kk) {
                 const uint64_t vm = vn_mask[kk];
@@ -828,7 +852,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     STAMP(ST_VNK);
                     psync();
                     STAMP(ST_VNK_WAIT);
-                    return;
+                    return false;
                 }
             }
             if constexpr (GATHER) {
@@ -880,6 +904,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                     STAMP(ST_VNK_WAIT);
                 }
             }
+            return false;
         };
         int it0 = 0;
         if (ALG == 0 && fast0) {
@@ -914,7 +939,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 if (head > 0) rowI[row0] = make_int2(pcnt + head, ppar ^ hpar ^ s_row0);
             }
             STAMP(ST_CN1);
-            psync();
+            split_local_sync();  // (no exit test in iteration 0)
             STAMP(ST_CN1_WAIT);
             r = row0;
             auto message0 = [&](int k, uint32_t mt, uint32_t mt2) {
@@ -929,7 +954,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message0(k, mt, 0u); });
             }
-            vn_phases();
+            vn_phases(0);
             had_vn = true;
             it0 = 1;
         }
@@ -1203,10 +1228,18 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
                 }
             }
             STAMP(ST_CN1);
-            psync();
+            // Split frames defer the exit test past the message pass (it writes
+            // only the stage: the totals the outputs read are untouched), to
+            // the barrier before the gather: one group barrier per iteration
+            // fewer, one wasted message pass on the last.  The message pass
+            // reads only rows its own wave scanned.
+            const bool defer = SPLIT && QL_SPLIT_DEFER && compute;
+            if (defer) split_local_sync();
+            else psync();
             STAMP(ST_CN1_WAIT);
-            const bool anymis = SPLIT ? (__hip_atomic_load(gmis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it + 1)
-                                      : (*s_flag == epoch);
+            const bool anymis =
+                defer || (SPLIT ? (__hip_atomic_load(gmis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it + 1)
+                                : (*s_flag == epoch));
             if constexpr (!SPA_FAM)
                 msclip = a.thr_on && (SPLIT || !had_vn || a.ms_clip_later || *s_big == epoch);
             // SPA: rp / t by div_rn_safe when every t of this wave came out of
@@ -1316,7 +1349,11 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
             } else {
                 meta.each_upto(epl, [&](int k, uint32_t mt) { message(k, mt, 0u); });
             }
-            vn_phases();
+            if (vn_phases(defer && check ? it + 1 : 0)) {
+                iters = ADAPT ? it + 1 : it;
+                okv = 1;
+                break;
+            }
             had_vn = true;
         }
 
@@ -1350,6 +1387,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
 #endif
 }
 #undef psync
+#undef split_local_sync
 
 // Palette + 2-bit codes of each frame's LLRs (one workgroup per frame).  Wave 0
 // collects up to 4 distinct values (bitwise) in first-occurrence order; a frame
