@@ -105,14 +105,14 @@ def test_relabelling_only_on_one_workgroup_register_shapes():
 def test_split_part_size_by_frames_per_xcd():
     """plan_v2_split (host planner, no GPU): parts of 16 waves (one per CU) or
     of 8 (two per CU, half the LDS), whichever runs more frames at once on an
-    XCD's 32 CUs.  C4 stand-in (307,200 edges): K = 8 x 16 waves, 4 frames per
-    XCD either way -> 16-wave parts.  C4 (ii) (409,600 edges): 11 x 16 waves
+    XCD's 32 CUs (ties: 8 waves).  C4 stand-in (307,200 edges): 8 x 16 waves
+    or 15 x 8, 4 frames per XCD either way -> 8-wave parts.  C4 (ii) (409,600 edges): 11 x 16 waves
     leave 10 CUs of an XCD waiting (2 frames), 21 x 8 waves run 3 -> 8-wave
     parts within 80 KiB of LDS each."""
     from conftest import load_fixture
 
     p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
-    assert p4["variant"] == "v2_split" and p4["lanes"] == 8 * 1024, p4
+    assert p4["variant"] == "v2_split" and p4["lanes"] == 15 * 512, p4
     g = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True)
     for alg in (Q.SPA, Q.OMSA):
         p = g.plan(0, alg)
@@ -122,6 +122,8 @@ def test_split_part_size_by_frames_per_xcd():
     try:
         p16 = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).plan(0, Q.SPA)
         assert p16["lanes"] == 11 * 1024, p16
+        p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
+        assert p4["lanes"] == 8 * 1024, p4
     finally:
         if old is None:
             os.environ.pop("QLDPC_SPLIT_WP")

@@ -349,18 +349,20 @@ def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec,
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-def test_c4_100k_split_half_parts(gpu_available, monkeypatch, alg, prim, sec):
-    """QLDPC_SPLIT_WP=8 (read when the graph is created): the C4 stand-in in
-    8-wave parts, two per CU (decoder_v2.hip PL = 512: LDS message slots at a
-    512-lane stride, the graph's per-part arrays at the 1024-lane stride with
-    waves 8..15 empty) — bit-exact with the oracle, posteriors included."""
+def test_c4_100k_split_full_parts(gpu_available, monkeypatch, alg, prim, sec):
+    """The C4 stand-in plans 8-wave parts, two per CU (decoder_v2.hip PL = 512:
+    LDS message slots at a 512-lane stride, the graph's per-part arrays at the
+    1024-lane stride with waves 8..15 empty; test_c4_100k_split_variant);
+    QLDPC_SPLIT_WP=16 (read when the graph is created) forces 16-wave parts,
+    one per CU — bit-exact with the oracle, posteriors included."""
     H = load_fixture("c4s_n102400_m32001.alist")
-    monkeypatch.setenv("QLDPC_SPLIT_WP", "8")
+    assert Q.Graph(H, host_only=True).plan(0, alg)["lanes"] == 15 * 512
+    monkeypatch.setenv("QLDPC_SPLIT_WP", "16")
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_WP")
     plan = g.plan(0, alg)
-    assert plan["lanes"] % 512 == 0 and plan["lanes"] >= 15 * 512, plan
-    assert plan["workgroups"] == 2 * 256, plan
+    assert plan["lanes"] == 8 * 1024, plan
+    assert plan["workgroups"] == 256, plan
     _, _, llr, synd = frames(H, 0.038, 8, 170 + alg)
     out = g.decode(Q.Params(alg, 12, True, 100.0, prim, sec), llr, synd, posterior=True)
     O = Oracle(H)
@@ -375,7 +377,8 @@ def test_c4_100k_split_half_parts(gpu_available, monkeypatch, alg, prim, sec):
 def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec, env):
     """The split layouts other than the default (read when the graph is
     created): the term-major stage (QLDPC_SPLIT_X=0, the A/B arm of
-    DecodeArgs::xoff) and K = 10 parts instead of the planner's 8 — same
+    DecodeArgs::xoff) and K = 10 parts of 16 waves instead of the planner's 15
+    of 8 — same
     bits, iterations and posteriors as the oracle and as the default graph."""
     H = load_fixture("c4s_n102400_m32001.alist")
     for k, v in env.items():
@@ -383,7 +386,7 @@ def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec,
     g0 = Q.Graph(H)
     for k in env:
         monkeypatch.delenv(k)
-    assert g0.plan(0, alg)["lanes"] == int(env.get("QLDPC_SPLIT_K", 8)) * 1024
+    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 15 * 512)
     _, _, llr, synd = frames(H, 0.038, 6, 90 + alg)
     p = Q.Params(alg, 10, True, 100.0, prim, sec)
     out0 = g0.decode(p, llr, synd, posterior=True)
