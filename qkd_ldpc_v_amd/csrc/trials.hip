@@ -39,10 +39,20 @@
 // k-prefix (kept: p goes to pbuf[i]), and a step at i >= k only writes
 // a[p] = i when p < k — the LAST such write wins, i.e. the largest i, which
 // the draw kernel keeps with an atomic max per prefix entry (last[p]).  The
-// finish kernel replays the k - 1 prefix swaps in order in LDS, takes last[p]
-// where set, and flips Bob's key at the k resulting positions.  The same
-// draws are consumed in the same order: the keys are the reference's bit for
-// bit.
+// finish kernel resolves the k - 1 prefix swaps (below), takes last[p] where
+// set, and flips Bob's key at the k resulting positions.  The same draws are
+// consumed in the same order: the keys are the reference's bit for bit.
+//
+// The prefix swaps are the inside-out shuffle: step i puts the value i at p_i
+// and moves the old a[p_i] to i.  So position x ends holding the last step
+// i > x with p_i = x (a "writer" of x) if there is one; otherwise the value
+// its own step x moved in, i.e. what position p_x held just before step x —
+// the last writer of p_x below x, or failing one, what p_x's own step moved
+// in, and so on down a chain of decreasing positions (x = 0, or a step with
+// p_y = y, ends it with the position itself).  With every position's writers
+// listed, each prefix position is resolved independently: the finish kernel
+// walks the k chains in parallel (expected chain length O(log k)) instead of
+// replaying k - 1 dependent LDS swaps on one thread.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -61,6 +71,7 @@ namespace {
 constexpr int kUnit = 128;      // draws per jump-table unit (one wave runs one segment of 64 trials)
 constexpr int kAliceUnits = 4;  // units per segment in Alice's part of the stream
 constexpr uint32_t kPrefixLds = 16384;  // k-prefix entries the finish kernel keeps in LDS (a and p: 128 KiB)
+constexpr uint32_t kParLds = 12288;     // ... for the parallel replay (p, writer lists: 3k + 1 words, 144 KiB)
 
 struct Xoshiro256pp {
     uint64_t s0, s1, s2, s3;
@@ -303,7 +314,94 @@ __global__ void __launch_bounds__(64) trials_draw_kernel(int n, uint32_t k, int 
     }
 }
 
-// Finish kernel, one workgroup per trial: replay the prefix swaps, merge the
+// The parallel prefix resolution (file header), one workgroup of 256 per
+// trial, k <= kParLds: p (k words), the writer lists in CSR form (offsets
+// k + 1, entries k), all in LDS.
+__device__ void finish_parallel(uint32_t k, int f, const TrialWs &W, const uint32_t *__restrict__ ws, uint32_t *sh,
+                                const uint8_t *__restrict__ alice, uint8_t *__restrict__ bob, int n) {
+    __shared__ uint32_t part[256];
+    const uint32_t tid = threadIdx.x, T = blockDim.x;
+    uint32_t *pl = sh, *off = sh + k, *lst = sh + 2 * k + 1;
+    for (uint32_t j = tid; j < k; j += T) {
+        pl[j] = j ? ws[W.pbuf() + (size_t)j * W.BP + f] : 0u;
+        off[j] = 0u;
+    }
+    __syncthreads();
+    for (uint32_t j = 1 + tid; j < k; j += T) {  // writer counts (p_j < j: j writes p_j)
+        const uint32_t p = pl[j];
+        if (p < j) atomicAdd(off + p, 1u);
+    }
+    __syncthreads();
+    // inclusive scan of the counts: a contiguous chunk per thread, the 256
+    // chunk sums scanned by wave 0 (four per lane)
+    const uint32_t C = (k + T - 1) / T, b0 = min(k, tid * C), b1 = min(k, b0 + C);
+    uint32_t sum = 0;
+    for (uint32_t i = b0; i < b1; ++i) sum += off[i];
+    part[tid] = sum;
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t v0 = part[4 * tid], v1 = part[4 * tid + 1], v2 = part[4 * tid + 2], v3 = part[4 * tid + 3];
+        const uint32_t tot = v0 + v1 + v2 + v3;
+        uint32_t inc = tot;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(inc, d, 64);
+            if ((int)tid >= d) inc += o;
+        }
+        const uint32_t ex = inc - tot;  // exclusive prefix of the lane's four chunks
+        part[4 * tid] = ex;
+        part[4 * tid + 1] = ex + v0;
+        part[4 * tid + 2] = ex + v0 + v1;
+        part[4 * tid + 3] = ex + v0 + v1 + v2;
+    }
+    __syncthreads();
+    uint32_t run = part[tid];
+    for (uint32_t i = b0; i < b1; ++i) {
+        run += off[i];
+        off[i] = run;
+    }
+    __syncthreads();
+    if (tid == 0) off[k] = off[k - 1];  // the entry count (end of the last list)
+    __syncthreads();
+    // fill from the back: off[p] ends at the start of p's list
+    for (uint32_t j = 1 + tid; j < k; j += T) {
+        const uint32_t p = pl[j];
+        if (p < j) lst[atomicSub(off + p, 1u) - 1u] = j;
+    }
+    __syncthreads();
+    const uint32_t *last = ws + W.last() + (size_t)f * W.k;
+    const uint8_t *ap = alice + (size_t)f * (size_t)n;
+    uint8_t *bp = bob + (size_t)f * (size_t)n;
+    for (uint32_t x = tid; x < k; x += T) {
+        uint32_t cur = x, bound = k, val;
+        for (;;) {
+            uint32_t best = 0;  // (writers are >= 1)
+            for (uint32_t q = off[cur], qe = off[cur + 1]; q < qe; ++q) {
+                const uint32_t i = lst[q];
+                best = (i < bound && i > best) ? i : best;
+            }
+            if (best) {
+                val = best;
+                break;
+            }
+            if (cur == 0) {
+                val = 0;
+                break;
+            }
+            const uint32_t p = pl[cur];
+            if (p == cur) {
+                val = cur;
+                break;
+            }
+            bound = cur;
+            cur = p;
+        }
+        const uint32_t lw = last[x];
+        const uint32_t pos = lw ? lw : val;
+        bp[pos] = (uint8_t)(ap[pos] ^ 1u);
+    }
+}
+
+// Finish kernel, one workgroup per trial: resolve the prefix swaps, merge the
 // last writers, flip Bob's key at the k chosen positions.  A trial with a
 // rejected shuffle draw (or every trial under force_serial) reruns its
 // shuffle and punctured draws sequentially from the state after Alice's bits.
@@ -316,10 +414,15 @@ __global__ void __launch_bounds__(256) trials_finish_kernel(int n, uint32_t k, i
     extern __shared__ uint32_t sh[];
     const int f = blockIdx.x;
     const TrialWs W(k, batch);
+    const bool serial0 = force_serial == 1 || ws[W.flag() + f] != 0u;
+    if (!serial0 && k <= kParLds && force_serial != 2) {
+        finish_parallel(k, f, W, ws, sh, alice, bob, n);
+        return;
+    }
     const bool in_lds = k <= kPrefixLds;
     uint32_t *a = in_lds ? sh : ws + W.abuf() + (size_t)f * W.k;
     uint32_t *pl = in_lds ? sh + k : nullptr;  // this trial's pbuf column, staged
-    const bool serial = force_serial || ws[W.flag() + f] != 0u;
+    const bool serial = serial0;
     for (uint32_t j = threadIdx.x; j < k; j += blockDim.x) {
         a[j] = j;
         if (pl && !serial) pl[j] = j ? ws[W.pbuf() + (size_t)j * W.BP + f] : 0u;
@@ -655,10 +758,13 @@ hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds
                        scratch);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // QLDPC_TRIAL_SERIAL=1: every trial takes the sequential rerun (the path a
-    // rejected draw takes), for the parity tests
+    // rejected draw takes), =2: the one-thread replay of the prefix swaps (the
+    // path of kParLds < k <= kPrefixLds); both for the parity tests
     const char *env = std::getenv("QLDPC_TRIAL_SERIAL");
-    const int force_serial = env && std::strcmp(env, "1") == 0;
-    const size_t lds = n_err <= kPrefixLds ? 2 * (size_t)n_err * sizeof(uint32_t) : 0;
+    const int force_serial = !env ? 0 : std::strcmp(env, "1") == 0 ? 1 : std::strcmp(env, "2") == 0 ? 2 : 0;
+    const size_t lds = n_err <= kParLds      ? (3 * (size_t)n_err + 1) * sizeof(uint32_t)
+                       : n_err <= kPrefixLds ? 2 * (size_t)n_err * sizeof(uint32_t)
+                                             : 0;
     if (lds > 65536 && (e = hipFuncSetAttribute(reinterpret_cast<const void *>(trials_finish_kernel),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
         return e;

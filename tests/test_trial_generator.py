@@ -242,10 +242,13 @@ def test_seed_sequences_agree():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,qber,batch", [(1024, 0.013, 24), (1024, 0.0015, 130), (10240, 0.0215, 24),
-                                           (10241, 0.05, 24), (102400, 0.038, 4)])
+                                           (10241, 0.05, 24), (102400, 0.038, 4), (102400, 0.13, 2),
+                                           (102400, 0.2, 2)])
 def test_device_trials_bitexact(gpu_available, n, qber, batch):
     """(batch 130: three groups of 64 trials, the last partial; n = 10241 and
-    1024 with batch 24: the byte-store path and a single segment group)"""
+    1024 with batch 24: the byte-store path and a single segment group; the
+    finish kernel resolves k <= 12288 prefix swaps in parallel, replays
+    k = 13312 on one thread in LDS and k = 20480 in global memory)"""
     import torch
 
     seeds = Q.trial_seeds(9012025, batch)
@@ -262,14 +265,17 @@ def test_device_trials_bitexact(gpu_available, n, qber, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("n,qber,batch,n_punct", [(10240, 0.0215, 70, 0), (1023, 0.05, 5, 0), (10240, 0.0156, 9, 37)])
-def test_device_trials_serial_rerun_bitexact(gpu_available, monkeypatch, n, qber, batch, n_punct):
+def test_device_trials_serial_rerun_bitexact(gpu_available, monkeypatch, n, qber, batch, n_punct, mode):
     """QLDPC_TRIAL_SERIAL=1 sends every trial through the finish kernel's
     sequential rerun — the path a trial with a rejected shuffle draw takes —
-    which must give the same keys and punctured draws as the oracle."""
+    and =2 through the one-thread replay of the prefix swaps (the path of
+    12288 < k <= 16384) instead of the parallel resolution: both must give
+    the same keys and punctured draws as the oracle."""
     import torch
 
-    monkeypatch.setenv("QLDPC_TRIAL_SERIAL", "1")
+    monkeypatch.setenv("QLDPC_TRIAL_SERIAL", mode)
     seeds = Q.trial_seeds(1022025, batch)
     d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()
     da = torch.empty((batch, n), dtype=torch.uint8, device="cuda")
