@@ -321,6 +321,21 @@ def test_c4_100k_split_full_decode(gpu_available):
     assert out.iterations.min() < 50
 
 
+@pytest.mark.parametrize("max_it,qber", [(1, 0.038), (2, 0.038), (3, 0.038), (50, 1e-6), (50, 0.003)])
+@pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
+def test_c4_split_deferred_exit_edges(gpu_available, alg, prim, sec, max_it, qber):
+    """Split frames test for the exit after the message pass (decoder_v2.hip
+    QL_SPLIT_DEFER; the frame leaves before the gather with the totals of the
+    scan that found it done).  Edges: iteration caps 1-3 (the last iteration
+    a scan only), frames without errors (AOMSA exits in iteration 0, SPA /
+    OMSA in iteration 1) and frames that converge in a few iterations —
+    bits, iterations, syndromes_match and posteriors vs the oracle."""
+    out, oi = assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=qber, batch=4, max_it=max_it,
+                            seed=700 + max_it)
+    if qber < 1e-5:
+        assert out.synd_ok.all()
+
+
 @pytest.mark.parametrize("wp", [0, 16])
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
 def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec, wp):
