@@ -142,10 +142,12 @@ asan-check: asan
 .PHONY: asan asan-check
 
 # A/B experiment build: `make ab AB=name AB_FLAGS=-D...` -> qkd_ldpc_v_amd/ab/name/
+# (AB_CAPI=1: capi.hip with the same flags too, for shapes the planner shares)
 # (selected at run time with QLDPC_AB_BUILD=name; never the product)
 AB ?= x
 ab:
 	mkdir -p $(PKG)/ab/$(AB)
 	$(HIPCC) $(HIPFLAGS) $(V2FLAGS) $(AB_FLAGS) -c $(CSRC)/decoder_v2.hip -o $(PKG)/ab/$(AB)/decoder_v2.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/order.o $(CSRC)/capi.o $(CSRC)/loaders.o $(CSRC)/relabel.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
+	if [ -n "$(AB_CAPI)" ]; then $(HIPCC) $(HIPFLAGS) $(AB_FLAGS) -c $(CSRC)/capi.hip -o $(PKG)/ab/$(AB)/capi.o; else cp $(CSRC)/capi.o $(PKG)/ab/$(AB)/capi.o; fi
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(PKG)/ab/$(AB)/decoder_v2.o $(CSRC)/decoder.o $(CSRC)/trials.o $(CSRC)/order.o $(PKG)/ab/$(AB)/capi.o $(CSRC)/loaders.o $(CSRC)/relabel.o -lz -o $(PKG)/ab/$(AB)/libqkdldpc_hip.so
 .PHONY: ab

@@ -585,19 +585,19 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
     const int wforce = env_int("QLDPC_SPLIT_WP", 0);
     if (wforce && wforce != 16 && wforce != 8) return false;
     auto smallest_k = [&](int WR) -> int {
-        const long long cap_part = (long long)WR * 64 * V2_R_TIGHT;
+        const long long cap_part = (long long)WR * 64 * V2_R_SPLIT;
         const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
-        if (kforce) return (kforce >= kmin && kforce <= 32 && attempt(kforce, V2_R_TIGHT, WR)) ? kforce : 0;
+        if (kforce) return (kforce >= kmin && kforce <= 32 && attempt(kforce, V2_R_SPLIT, WR)) ? kforce : 0;
         for (int K = kmin; K <= 32; ++K)
-            if (attempt(K, V2_R_TIGHT, WR)) return K;
+            if (attempt(K, V2_R_SPLIT, WR)) return K;
         return 0;
     };
     const int k16 = (wforce == 8) ? 0 : smallest_k(16);
     const int k8 = (wforce == 16) ? 0 : smallest_k(8);
     const int f16 = k16 ? 32 / k16 : 0, f8 = k8 ? 64 / k8 : 0;
     if (!k16 && !k8) return false;
-    if (k8 && (f8 >= f16 || !k16)) return attempt(k8, V2_R_TIGHT, 8);  // (the last attempt sets the plan)
-    return attempt(k16, V2_R_TIGHT, 16);
+    if (k8 && (f8 >= f16 || !k16)) return attempt(k8, V2_R_SPLIT, 8);  // (the last attempt sets the plan)
+    return attempt(k16, V2_R_SPLIT, 16);
 }
 
 template <typename T>

@@ -31,6 +31,10 @@ enum Variant : int {
 // waves, holds no more edges than 56 x 12 and its SPA build falls back to a
 // scratch array, so it is not built.)
 constexpr int V2_R_TIGHT = 40, V2_R_SMALL = 44, V2_R_MID = 56;
+#ifndef QL_SPLIT_R
+#define QL_SPLIT_R 40  // split frames' slots per lane (A/B: 44, 48 with a matching capi build)
+#endif
+constexpr int V2_R_SPLIT = QL_SPLIT_R;
 constexpr int V2_CODES_CAP = 20480;  // V2: bits per frame whose palette indices fit LDS (n <= this)
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;

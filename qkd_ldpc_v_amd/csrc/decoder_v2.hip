@@ -1487,14 +1487,14 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
 KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl, int pl = REG_TSTRIDE) {
     if (split_k > 1 && pl == REG_TSTRIDE / 2) {
         constexpr int H = REG_TSTRIDE / 2;
-        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT, false, false, H>
-                                : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT, false, false, H>;
-        return pick_v2<V2_R_TIGHT, 0, true, H>(alg);
+        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, 0, true, V2_RL_SPLIT, false, false, H>
+                                : decode_v2_kernel<1, V2_R_SPLIT, 0, true, V2_RL_SPLIT, false, false, H>;
+        return pick_v2<V2_R_SPLIT, 0, true, H>(alg);
     }
     if (split_k > 1) {
-        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, true, V2_RL_SPLIT>
-                                : decode_v2_kernel<1, V2_R_TIGHT, 0, true, V2_RL_SPLIT>;
-        return pick_v2<V2_R_TIGHT, 0, true>(alg);
+        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, 0, true, V2_RL_SPLIT>
+                                : decode_v2_kernel<1, V2_R_SPLIT, 0, true, V2_RL_SPLIT>;
+        return pick_v2<V2_R_SPLIT, 0, true>(alg);
     }
     if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, false, V2_RL> : decode_v2_kernel<1, V2_R_TIGHT, 0, false, V2_RL>;
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
