@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 O=gpurun_out/r05_r44; mkdir -p $O
 for arm in r44; do
-  QLDPC_AB_BUILD=$arm timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "c4 or split" > $O/pytest_$arm.log 2>&1 || { tail -30 $O/pytest_$arm.log; exit 10; }
+  QLDPC_AB_BUILD=$arm timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "c4 or split" > $O/pytest_$arm.log 2>&1; grep -E "^FAILED" $O/pytest_$arm.log | cut -c1-120
   echo "$arm $(tail -1 $O/pytest_$arm.log)"
 done
 for rep in 1 2; do
