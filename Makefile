@@ -143,7 +143,7 @@ asan-check: asan
 
 # A/B experiment build: `make ab AB=name AB_FLAGS=-D...` -> qkd_ldpc_v_amd/ab/name/
 # (AB_CAPI=1: capi.hip with the same flags too, for shapes the planner shares)
-# (selected at run time with QLDPC_AB_BUILD=name; never the product)
+# (selected at run time with QLDPC_DIAG=1 QLDPC_AB_BUILD=name; never the product)
 AB ?= x
 ab:
 	mkdir -p $(PKG)/ab/$(AB)

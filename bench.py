@@ -9,14 +9,21 @@ trials (synthetic BSC keys) are generated before timing and are resident in HBM.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c1|c4]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Frames are sharded across ranks with no data-path collective (weak scaling:
-every GPU decodes its own batch); a barrier + max-over-ranks bracket the timed
-region.  Rank 0 prints one JSON line.
+One process per GPU.  `--gpus N > 1` without a launcher starts the N ranks
+itself (child processes, before this process touches the GPU) with the same
+environment torchrun would give them; under a launcher WORLD_SIZE must equal
+N.  Either way the run exits non-zero when the node has fewer than N GPUs, so
+`--gpus N` never silently measures fewer ranks.  Frames are sharded across
+ranks with no data-path collective (weak scaling: every GPU decodes its own
+batch); a barrier + max-over-ranks bracket the timed region.  Rank 0 prints
+one JSON line.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -100,20 +107,38 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c5-point", type=int, default=-1,
                     help="with --workload c5ra: one of the 26 C5 sweep points (C5_POINTS index)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="test only: every rank on device 0 (logical devices), gloo for the bracket collectives "
+                         "(RCCL refuses two ranks on one GPU); the line's timing is then not a node figure")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
 
     import torch
 
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        # no launcher: start the N ranks here, before any GPU call in this process
+        check_devices(torch.cuda.device_count(), args.gpus, args.share_device)
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher disagrees with --gpus {args.gpus}")
+    check_devices(torch.cuda.device_count(), world, args.share_device)
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if launched:  # also at WORLD_SIZE 1 (torchrun --nproc-per-node 1): the same bracket and combine
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import qkd_ldpc_v_amd as Q
 
@@ -247,7 +272,8 @@ def main():
     it_sum = int(last.iters.to(torch.int64).sum().item())
     n_ok = int(last.ok.to(torch.int64).sum().item())
     n_keys = int(last.km.to(torch.int64).sum().item())
-    tot = combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, batch, kernel_ms or 0.0, dev)
+    tot = combine_ranks(dist, elapsed, it_sum, n_ok, n_keys, batch, kernel_ms or 0.0,
+                        torch.device("cpu") if args.share_device else dev)
     elapsed_max, kernel_ms_max = tot["elapsed_max"], tot["kernel_ms_max"]
     it_total, ok_total, keys_total, frames_step = tot["iters"], tot["ok"], tot["keys"], tot["frames"]
 
@@ -295,7 +321,9 @@ def main():
                 "workload": desc, "matrix": fixture or "generated: regular_code(102400, 22001, 4, 777)", "n": n, "m": m, "edges": E, "info_bits_per_frame": k_info,
                 "algorithm": Q.ALGORITHM_NAMES[alg], "qber": qber, "max_iterations": args.max_iterations,
                 "batch_per_gpu": batch, "global_batch": int(frames_step),
-                "parallelism": f"frames sharded over {world} GPU(s), no collectives",
+                "parallelism": (f"frames sharded over {world} ranks on ONE GPU (--share-device test run), "
+                                "no collectives" if args.share_device else
+                                f"frames sharded over {world} GPU(s), no collectives"),
                 "kernel_variant": plan["variant"], "lanes_per_frame": plan["lanes"], "streams": nst,
                 "edges_per_lane": plan["edges_per_lane"], "workgroups": plan["workgroups"],
             },
@@ -347,6 +375,49 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def check_devices(have: int, need: int, shared: bool) -> None:
+    """Refuse a run that would measure fewer GPUs than asked for."""
+    if have < (1 if shared else need):
+        raise SystemExit(f"bench.py: --gpus {need} needs {need} GPUs, this node has {have}")
+
+
+def rank_env(base: dict, world: int, rank: int, port: int) -> dict:
+    """The environment torch.distributed.run gives rank `rank` of a one-node job."""
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(world: int, cmd: list, base_env=None) -> int:
+    """Run `cmd` as ranks 0..world-1 (child processes, one per GPU) and wait
+    for all of them.  If one fails, the others are terminated (they would wait
+    at the barrier forever).  Returns the first non-zero exit code, else 0."""
+    port = free_port()
+    base = dict(os.environ if base_env is None else base_env)
+    procs = [subprocess.Popen(cmd, env=rank_env(base, world, r, port)) for r in range(world)]
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def rank_trial_seeds(Q, sim_seed: int, batch: int, world: int, rank: int):

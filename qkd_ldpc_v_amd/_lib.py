@@ -15,11 +15,16 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqkdldpc_hip.so")
-if os.environ.get("QLDPC_DIAG_STAMPS") == "1":  # diagnostic phase-stamp build (Makefile target `stamps`)
+# Alternative builds are selected only under the diagnostic switch QLDPC_DIAG=1
+# (the library reads its A/B knobs under the same switch): without it the
+# product library is loaded whatever else the environment holds.
+DIAG = os.environ.get("QLDPC_DIAG") == "1"
+_AB_BUILD = os.environ.get("QLDPC_AB_BUILD") if DIAG else None
+if DIAG and os.environ.get("QLDPC_DIAG_STAMPS") == "1":  # diagnostic phase-stamp build (Makefile target `stamps`)
     LIB_PATH = os.path.join(_HERE, "diag", "libqkdldpc_hip.so")
-if os.environ.get("QLDPC_AB_BUILD"):  # A/B experiments: an alternative in-tree build, qkd_ldpc_v_amd/ab/<name>/
-    LIB_PATH = os.path.join(_HERE, "ab", os.environ["QLDPC_AB_BUILD"], "libqkdldpc_hip.so")
-if os.environ.get("QLDPC_ASAN") == "1":  # `make asan`: host code under ASan + UBSan (build/asan/)
+if _AB_BUILD:  # A/B experiments: an alternative in-tree build, qkd_ldpc_v_amd/ab/<name>/
+    LIB_PATH = os.path.join(_HERE, "ab", _AB_BUILD, "libqkdldpc_hip.so")
+if DIAG and os.environ.get("QLDPC_ASAN") == "1":  # `make asan`: host code under ASan + UBSan (build/asan/)
     LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "asan", "libqkdldpc_hip.so")
 
 QLDPC_OK = 0
@@ -123,7 +128,7 @@ def lib() -> ctypes.CDLL:
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGNATURES.items():
             fn = getattr(L, name, None)
-            if fn is None and os.environ.get("QLDPC_AB_BUILD"):
+            if fn is None and _AB_BUILD:
                 continue  # an older A/B build may predate an entry point
             if fn is None:
                 raise ImportError(f"{LIB_PATH} does not export {name}: rebuild it (make)")

@@ -91,6 +91,8 @@ struct HostIO {  // device staging buffers of the host-buffer entry
 // decodes on the other stream).
 struct TrialSlot {
     hipStream_t stream = nullptr;
+    // the chunk's window: ev0 (after its trials are generated and the other
+    // slot's chunk has ended) .. ev1 (after the key compare)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     uint64_t *seeds = nullptr, *clk = nullptr;
     uint8_t *alice = nullptr, *bob = nullptr, *palice = nullptr, *pbob = nullptr, *alice_ext = nullptr;
@@ -237,8 +239,22 @@ size_t lds_of(const qldpc_graph &g, int alg) {
                                : lds_bytes_for(g.variant, g.n, g.m, g.T);
 }
 
+}  // namespace
+
+// The planner's and the launches' A/B knobs (QLDPC_SPLIT_K, QLDPC_VNG, ...)
+// are read only under the diagnostic switch QLDPC_DIAG=1: without it the
+// product ignores every QLDPC_* tuning variable, so a stray variable in a
+// user's environment cannot change the plan the reference's driver gets.
+const char *qldpc::qldpc_diag_env(const char *name) {
+    const char *d = std::getenv("QLDPC_DIAG");
+    if (!d || std::strcmp(d, "1") != 0) return nullptr;
+    return std::getenv(name);
+}
+
+namespace {
+
 int env_int(const char *name, int dflt) {
-    const char *v = std::getenv(name);
+    const char *v = qldpc_diag_env(name);
     return (v && *v) ? std::atoi(v) : dflt;
 }
 
@@ -492,8 +508,10 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
         if (row_ptr[j + 1] == row_ptr[j]) return false;
     const long long E = g.E;
     const int WP = REG_TSTRIDE / 64;  // waves per part in the graph's arrays
-    // One attempt: K parts of WR waves, R slots per lane.
-    auto attempt = [&](int K, int R, int WR) -> bool {
+    // One attempt: K parts of WR waves, V2_R_SPLIT slots per lane in VGPRs /
+    // LDS plus RG in per-workgroup global scratch.
+    auto attempt = [&](int K, int RG, int WR) -> bool {
+        const int R = V2_R_SPLIT + RG;
         const int PL = WR * 64;                                  // the part's lanes (threads)
         const size_t LIM = (size_t)LDS_LIMIT * WR / WP;           // its LDS: 1 or 2 parts per CU
         const int W = WP * K, Wr = WR * K;
@@ -560,8 +578,8 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
             }
         }
         g.variant = VAR_V2;
-        g.v2R = R;
-        g.v2RG = 0;
+        g.v2R = V2_R_SPLIT;
+        g.v2RG = RG;
         g.T = W * 64;
         g.EPL = epl;
         g.wave_rows = rb;
@@ -581,23 +599,48 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
     // as fast as 8 x 16 and the step runs 4% faster, profiles/r05/c4_wp.txt).  (K need not divide an XCD's parts:
     // groups form in claim order and a workgroup joins the next group whenever
     // it finishes a frame.)
+    //
+    // Scratch message slots (RG = V2_RG_SPLIT, round 6): 52 slots per lane
+    // instead of 40 cut the parts per frame by ~1/4, at a cost — each part's
+    // passes hold ~1.3x the edges and the scratch slots travel through L2 —
+    // measured at 1.22-1.33x per frame-iteration (profiles/r06/split_rg/): C4
+    // (ii) 21 -> 16 parts, 3 -> 4 frames per XCD, decode -8%; the stand-in
+    // 15 -> 12 parts, 4 -> 5 frames, +6%.  So the planner takes them only when
+    // they raise frames per XCD by at least 4/3.  QLDPC_SPLIT_SCRATCH=0 / 1
+    // (diagnostic) forces them off / on.
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
     const int wforce = env_int("QLDPC_SPLIT_WP", 0);
+    const int sforce = env_int("QLDPC_SPLIT_SCRATCH", -1);
     if (wforce && wforce != 16 && wforce != 8) return false;
-    auto smallest_k = [&](int WR) -> int {
-        const long long cap_part = (long long)WR * 64 * V2_R_SPLIT;
+    auto smallest_k = [&](int WR, int RG) -> int {
+        const long long cap_part = (long long)WR * 64 * (V2_R_SPLIT + RG);
         const int kmin = (int)std::max<long long>(2, (E + cap_part - 1) / cap_part);
-        if (kforce) return (kforce >= kmin && kforce <= 32 && attempt(kforce, V2_R_SPLIT, WR)) ? kforce : 0;
+        if (kforce) return (kforce >= kmin && kforce <= 32 && attempt(kforce, RG, WR)) ? kforce : 0;
         for (int K = kmin; K <= 32; ++K)
-            if (attempt(K, V2_R_SPLIT, WR)) return K;
+            if (attempt(K, RG, WR)) return K;
         return 0;
     };
-    const int k16 = (wforce == 8) ? 0 : smallest_k(16);
-    const int k8 = (wforce == 16) ? 0 : smallest_k(8);
-    const int f16 = k16 ? 32 / k16 : 0, f8 = k8 ? 64 / k8 : 0;
-    if (!k16 && !k8) return false;
-    if (k8 && (f8 >= f16 || !k16)) return attempt(k8, V2_R_SPLIT, 8);  // (the last attempt sets the plan)
-    return attempt(k16, V2_R_SPLIT, 16);
+    struct Choice {
+        int K = 0, WR = 0, RG = 0, f = 0;
+    };
+    // per slot budget: the smallest K of each part size, then the size that
+    // runs more frames per XCD at once (32 CUs: 32 parts of 16 waves or 64 of
+    // 8; ties: 8 waves)
+    auto best_for = [&](int RG) -> Choice {
+        const int k16 = (wforce == 8) ? 0 : smallest_k(16, RG);
+        const int k8 = (wforce == 16) ? 0 : smallest_k(8, RG);
+        const int f16 = k16 ? 32 / k16 : 0, f8 = k8 ? 64 / k8 : 0;
+        Choice c;
+        if (k8 && (f8 >= f16 || !k16)) c = {k8, 8, RG, f8};
+        else if (k16) c = {k16, 16, RG, f16};
+        return c;
+    };
+    const Choice c0 = sforce == 1 ? Choice{} : best_for(0);
+    const Choice cs = sforce == 0 ? Choice{} : best_for(V2_RG_SPLIT);
+    Choice pick = c0;
+    if (cs.K && (!c0.K || sforce == 1 || 3 * cs.f >= 4 * c0.f)) pick = cs;
+    if (!pick.K) return false;
+    return attempt(pick.K, pick.RG, pick.WR);  // (the last attempt sets the plan)
 }
 
 template <typename T>
@@ -705,7 +748,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
     }
     if (g->dv_max >= MAX_DV) return fail(QLDPC_EUNSUP, "a bit node has degree >= 511");
     // QLDPC_VARIANT=v1 keeps the first-generation planner (comparison / tests).
-    const char *want = std::getenv("QLDPC_VARIANT");
+    const char *want = qldpc_diag_env("QLDPC_VARIANT");
     const bool v1_only = want && std::strcmp(want, "v1") == 0;
     if (g->paired && want && std::strcmp(want, "v2") == 0)
         return fail(QLDPC_EUNSUP, "QLDPC_VARIANT=v2 but the adjacency needs occurrence pairing (v1)");
@@ -1141,7 +1184,7 @@ int build_graph(int32_t n, int32_t m, const int32_t *row_ptr, const int32_t *col
         assign(meta_ms, meta2_ms, xbit_ms);
     }
     g->nst_max = row_sem.empty() ? 0 : nst_max;
-    if (v2 && std::getenv("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
+    if (v2 && qldpc_diag_env("QLDPC_DEBUG_PLAN")) {  // host-side plan statistics on stderr
         auto visited = [&](const std::vector<uint64_t> &v) {
             long long s = 0;
             for (int w = 0; w < W; ++w)
@@ -1271,7 +1314,9 @@ long long v2_llr_lab_offset(const qldpc_graph &g) {
 }
 
 long long v2_scratch_doubles(const qldpc_graph &g) {
-    if (g.split_k > 1) return 32;  // the stage is per frame (Workspace::gstage)
+    // split frames: the stage is per frame (Workspace::gstage); only the
+    // scratch message slots (V2_RG_SPLIT, an A/B arm) are per workgroup
+    if (g.split_k > 1) return g.v2RG > 0 ? (long long)g.v2RG * REG_TSTRIDE : 32;
     long long end = g.rows_global_ms ? v2_rows_offset(g) + 2LL * g.m
                                      : (long long)g.v2RG * REG_TSTRIDE + g.stage_doubles;
     if (v2_llr_lab_offset(g) >= 0) end = v2_llr_lab_offset(g) + g.n;
@@ -1295,6 +1340,39 @@ int ensure_codes(qldpc_graph *g, Workspace *w, int batch, hipStream_t stream) {
     HIP_TRY(hipMalloc(&w->pal_ok, (size_t)batch));
     w->code_frames = (size_t)batch;
     return QLDPC_OK;
+}
+
+// The device frame builders stage the frame's keys in LDS as bit words
+// (decoder.hpp build_frames_lds / build_frames_ra_lds): refuse larger graphs
+// with a message instead of a launch error.  (Plain frames: n <= 655,360;
+// rate-adapted: n <= ~436k; the reference's codes stop at n = 102,400.)
+int frame_builder_fits(const qldpc_graph *g, int n_punct /* < 0: plain frames */) {
+    const size_t lds = n_punct < 0 ? build_frames_lds(g->n) : build_frames_ra_lds(g->n, n_punct);
+    if (lds <= LDS_MAX_BYTES) return QLDPC_OK;
+    return fail(QLDPC_EUNSUP, "n = " + std::to_string(g->n) + ": the device frame builder keeps the frame's keys in " +
+                                  "LDS (" + std::to_string(lds) + " bytes > " + std::to_string(LDS_MAX_BYTES) +
+                                  "); decode such frames through qldpc_decode_batch[_device] with host-built LLRs");
+}
+
+// Split frames: at most one split decode in flight per physical device.  A
+// part group forms from workgroups of ONE launch resident on one XCD; two
+// persistent split launches (two streams of one graph, two graphs, logical
+// devices) that are each only partly resident could wait on each other's
+// workgroups until the group timeout.  Each split launch therefore waits (on
+// the GPU, hipStreamWaitEvent) for the previous one on its device to end;
+// one-workgroup frames have no such coupling and still overlap.
+struct SplitSerial {
+    std::mutex mu;
+    hipEvent_t last = nullptr;
+    bool recorded = false;
+};
+SplitSerial &split_serial(int device) {
+    static std::mutex mu;
+    static std::map<int, std::unique_ptr<SplitSerial>> per_device;
+    std::lock_guard<std::mutex> lk(mu);
+    auto &p = per_device[device];
+    if (!p) p.reset(new SplitSerial);
+    return *p;
 }
 
 // Split frames: after the stream is idle, fail loudly if a part group timed
@@ -1462,7 +1540,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     a.codes = w->codes; a.palette = w->palette; a.pal_ok = w->pal_ok;
     a.n_iso = g->n_iso; a.iso_bits = dg->iso_bits; a.v2R = g->v2R; a.v2RG = g->v2RG;
     {  // min-sum bit gather where the shape allows it (QLDPC_VNG=0: VN phases instead)
-        const char *e = std::getenv("QLDPC_VNG");
+        const char *e = qldpc_diag_env("QLDPC_VNG");
         const bool off = e && std::strcmp(e, "0") == 0;
         if (v2 && g->vng && !off && v2_vng_ok(alg, g->v2R, g->v2RG, a.split_k, g->dv_max, g->m)) {
             a.vn_rows = reinterpret_cast<const uint2 *>(dg->vn_rows);
@@ -1481,7 +1559,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     {  // claim order: hardest-looking frames first (order.hip; QLDPC_ORDER=0: index order).
         // It only schedules — results never depend on it — so a shape it cannot
         // run (LDS beyond the device limit) decodes in index order instead.
-        const char *e = std::getenv("QLDPC_ORDER");
+        const char *e = qldpc_diag_env("QLDPC_ORDER");
         if (!(e && std::strcmp(e, "0") == 0) && batch > 1) {
             // (relabelled graphs: the frame codes are in label order, so is the row-ELL it reads)
             const hipError_t oe = launch_frame_order(g->n, g->m, dg->col_orig ? dg->ell_lab : dg->ell_col,
@@ -1501,6 +1579,14 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     HIP_TRY(hipMemsetAsync(d_st, 0, nst * sizeof(uint64_t), stream));
     a.stamps = d_st;
 #endif
+    std::unique_lock<std::mutex> split_lk;
+    SplitSerial *ser = nullptr;
+    if (v2 && g->split_k > 1) {  // one split decode in flight per device (above)
+        ser = &split_serial(dg->device);
+        split_lk = std::unique_lock<std::mutex>(ser->mu);
+        if (!ser->last) HIP_TRY(hipEventCreateWithFlags(&ser->last, hipEventDisableTiming));
+        if (ser->recorded) HIP_TRY(hipStreamWaitEvent(stream, ser->last, 0));
+    }
     if (g->kernel_timing) {  // (the workspace is per stream: no other call records on these events)
         if (!w->ev0) HIP_TRY(hipEventCreate(&w->ev0));
         if (!w->ev1) HIP_TRY(hipEventCreate(&w->ev1));
@@ -1508,6 +1594,11 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     }
     if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
     else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
+    if (ser) {
+        HIP_TRY(hipEventRecord(ser->last, stream));
+        ser->recorded = true;
+        split_lk.unlock();
+    }
     if (g->kernel_timing) {
         HIP_TRY(hipEventRecord(w->ev1, stream));
         w->ev_recorded = true;
@@ -1574,6 +1665,7 @@ int qkd_ldpc_window(qldpc_graph *g, DeviceGraph *dg, const qldpc_rate_plan *plan
             llr = w->llr_ws;
         }
     }
+    if (int r = frame_builder_fits(g, plan ? plan->n_punct : -1)) return r;
     if (plan)
         HIP_TRY(launch_build_frames_ra(g->n, g->m, dg->ell_col, dg->row_deg, pd->cls, pd->src, plan->n_punct, batch,
                                        d_alice, d_bob, d_punct_alice, d_punct_bob, d_log_p, d_alice_ext, llr,
@@ -1968,6 +2060,7 @@ int qldpc_build_frames_device(qldpc_graph *g, int32_t device, int32_t batch, con
         return fail(QLDPC_EINVAL, "NULL device buffer");
     DeviceGraph *dg = find_dev(g, device);
     if (!dg) return fail(QLDPC_EINVAL, "graph does not live on that device");
+    if (int r = frame_builder_fits(g, -1)) return r;
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
@@ -2262,6 +2355,7 @@ int qldpc_build_frames_rate_adapt_device(qldpc_graph *g, const qldpc_rate_plan *
     for (auto &d : plan->devs)
         if (d.device == device) pd = &d;
     if (!dg || !pd) return fail(QLDPC_EINVAL, "graph / plan does not live on that device");
+    if (int r = frame_builder_fits(g, plan->n_punct)) return r;
     int prev = 0;
     HIP_TRY(hipGetDevice(&prev));
     HIP_TRY(hipSetDevice(device));
@@ -2557,6 +2651,7 @@ int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const q
             for (int f = lo; f < hi && !r;) {
                 TrialSlot &t = dg->tslot[dg->next_slot];
                 dg->next_slot ^= 1;
+                const TrialSlot &o = dg->tslot[dg->next_slot];  // the other slot
                 (void)harvest_slot(g, dg, gi, t);  // (a previous chunk, possibly another job's)
                 const int nb = std::min(cap, hi - f);
                 if ((r = ensure(t, nb))) break;
@@ -2571,6 +2666,12 @@ int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const q
                     // run_trial's keys (+ QKD_LDPC_RATE_ADAPT's punctured draws), seed = seeds[n] + curr_sim (:743)
                     HIP_TRY(launch_trials(n, n_err, nb, t.seeds, seed_add, t.alice, t.bob, t.tscratch, n_punct,
                                           t.palice, t.pbob, t.stream));
+                    // Only trial generation overlaps the other slot's chunk (the
+                    // previous chunk, or the previous combination's under
+                    // qldpc_run_trials_submit): the frame build, decode and
+                    // compare wait for it to end, so two decodes never share
+                    // the CUs and a chunk's window [ev0, ev1] is its own work.
+                    if (o.nb > 0) HIP_TRY(hipStreamWaitEvent(t.stream, o.ev1, 0));
                     HIP_TRY(hipEventRecord(t.ev0, t.stream));
                     int rr = qkd_ldpc_window(g, dg, plan, p, nb, t.alice, t.bob, t.palice, t.pbob, t.logp, t.alice_ext,
                                              nullptr, t.synd, t.bits, t.iters, t.ok, t.km, t.stream, t.clk);

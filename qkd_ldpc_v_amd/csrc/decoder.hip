@@ -25,6 +25,9 @@
 //     edge that is the k-th edge of its bit.
 #include <float.h>
 
+#include <map>
+#include <mutex>
+
 #include "decoder_common.hpp"
 
 namespace qldpc {
@@ -450,11 +453,21 @@ long long scratch_doubles_for(int variant, int n, int m, int T, int EPL) {
     return d;
 }
 
+hipError_t allow_dynamic_lds(const void *k, size_t bytes) {
+    static std::mutex mu;
+    static std::map<const void *, size_t> limit;  // the largest value set per kernel
+    std::lock_guard<std::mutex> lk(mu);
+    size_t &cur = limit[k];
+    if (bytes <= cur) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) cur = bytes;
+    return e;
+}
+
 hipError_t launch_decode(int variant, const DecodeArgs &a, int workgroups, size_t lds_bytes,
                          hipStream_t stream) {
     KernelFn k = kernel_for(variant, a.alg);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(k), lds_bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(workgroups), dim3(a.T), lds_bytes, stream, a);
     return hipGetLastError();
@@ -462,8 +475,7 @@ hipError_t launch_decode(int variant, const DecodeArgs &a, int workgroups, size_
 
 hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
     KernelFn k = kernel_for(variant, alg);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(k), lds_bytes);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, T, lds_bytes);
 }
@@ -474,11 +486,10 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
                                const int32_t *col_orig, hipStream_t stream) {
     (void)max_dc;
     if (batch <= 0) return hipSuccess;
-    const size_t lds = 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t);  // the two keys as bit words
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds = build_frames_lds(n);  // the two keys as bit words
+    if (lds > LDS_MAX_BYTES) return hipErrorInvalidValue;
     if (lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(build_frames_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(build_frames_kernel), lds);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, alice,

@@ -35,6 +35,17 @@ constexpr int V2_R_TIGHT = 40, V2_R_SMALL = 44, V2_R_MID = 56;
 #define QL_SPLIT_R 40  // split frames' slots per lane (A/B: 44, 48 with a matching capi build)
 #endif
 constexpr int V2_R_SPLIT = QL_SPLIT_R;
+// Split frames may add this many message slots per lane in per-workgroup
+// global scratch to the V2_R_SPLIT register/LDS slots (round 6): more edges
+// per part, so fewer parts per frame and more frames per XCD.  The planner
+// takes them only when they raise frames per XCD by >= 4/3 (capi.hip
+// plan_v2_split).
+#ifndef QL_SPLIT_RG
+#define QL_SPLIT_RG 12
+#endif
+constexpr int V2_RG_SPLIT = QL_SPLIT_RG;
+static_assert(V2_RG_SPLIT > 0 && V2_RG_SPLIT % 4 == 0 && V2_R_SPLIT + V2_RG_SPLIT <= 64,
+              "split scratch slots: groups of four, <= 64 slots in all");
 constexpr int V2_CODES_CAP = 20480;  // V2: bits per frame whose palette indices fit LDS (n <= this)
 // Hybrid instantiation: 44 VGPR slots + this many slots in per-workgroup global scratch.
 constexpr int V2_RG_HYBRID = 20;
@@ -198,6 +209,23 @@ hipError_t launch_decode(int variant, const DecodeArgs &a, int workgroups, size_
 // Max resident workgroups per CU for (variant, alg, T, lds).
 hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_per_cu);
 
+// The environment variable `name` under the diagnostic switch QLDPC_DIAG=1, else NULL (capi.hip):
+// the only way the library reads its QLDPC_* A/B knobs.
+const char *qldpc_diag_env(const char *name);
+constexpr size_t LDS_MAX_BYTES = 160 * 1024;
+// Opt kernel k in to `bytes` of dynamic LDS (hipFuncAttributeMaxDynamicSharedMemorySize).
+// The limit per kernel only ever rises, under one process-wide mutex: a
+// per-launch value set by one thread could otherwise lower the limit between
+// another thread's set and its launch (decoder.hip).
+hipError_t allow_dynamic_lds(const void *k, size_t bytes);
+// Dynamic LDS of the frame builders: the keys (+ punctured draws, the extended
+// key) as bit words.  Beyond LDS_MAX_BYTES (plain frames: n > 655,360; rate-
+// adapted: n > ~436k) the entries refuse the graph with QLDPC_EUNSUP.
+inline size_t build_frames_lds(int n) { return 2 * (size_t)((n + 31) / 32) * sizeof(uint32_t); }
+inline size_t build_frames_ra_lds(int n, int n_punct) {
+    return (2 * (size_t)((n + 31) / 32) + (size_t)((n_punct + 31) / 32) + 2 * (size_t)((n + 63) / 64)) *
+           sizeof(uint32_t);
+}
 hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
                                int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,

@@ -1484,17 +1484,20 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
     }
 }
 
+// Split frames: parts of 16 or 8 waves (PL lanes), SG scratch slots (0 or V2_RG_SPLIT).
+template <int SG, int PL>
+KernelFn kernel_split(int alg, bool rl) {
+    if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, SG, true, V2_RL_SPLIT, false, false, PL>
+                            : decode_v2_kernel<1, V2_R_SPLIT, SG, true, V2_RL_SPLIT, false, false, PL>;
+    return pick_v2<V2_R_SPLIT, SG, true, PL>(alg);
+}
+
 KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl, int pl = REG_TSTRIDE) {
-    if (split_k > 1 && pl == REG_TSTRIDE / 2) {
-        constexpr int H = REG_TSTRIDE / 2;
-        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, 0, true, V2_RL_SPLIT, false, false, H>
-                                : decode_v2_kernel<1, V2_R_SPLIT, 0, true, V2_RL_SPLIT, false, false, H>;
-        return pick_v2<V2_R_SPLIT, 0, true, H>(alg);
-    }
     if (split_k > 1) {
-        if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, 0, true, V2_RL_SPLIT>
-                                : decode_v2_kernel<1, V2_R_SPLIT, 0, true, V2_RL_SPLIT>;
-        return pick_v2<V2_R_SPLIT, 0, true>(alg);
+        if (RG != 0 && RG != V2_RG_SPLIT) return nullptr;  // (no such instantiation)
+        if (pl == REG_TSTRIDE / 2)
+            return RG ? kernel_split<V2_RG_SPLIT, REG_TSTRIDE / 2>(alg, rl) : kernel_split<0, REG_TSTRIDE / 2>(alg, rl);
+        return RG ? kernel_split<V2_RG_SPLIT, REG_TSTRIDE>(alg, rl) : kernel_split<0, REG_TSTRIDE>(alg, rl);
     }
     if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_TIGHT, 0, false, V2_RL> : decode_v2_kernel<1, V2_R_TIGHT, 0, false, V2_RL>;
     if (RG > 0) return pick_v2<V2_R_SMALL, V2_RG_HYBRID>(alg);
@@ -1541,9 +1544,9 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
                                        a.split_k > 1 ? v2_use_rl_split(a.alg, a.n, a.split_mrows, a.split_cb, a.T)
                                                      : v2_use_rl(a.alg, a.v2R, a.v2RG, false, a.n, a.m, a.T),
                                        a.split_k > 1 ? a.T : REG_TSTRIDE);
+    if (!k) return hipErrorInvalidValue;
     if (a.split_k > 1 && a.T != REG_TSTRIDE && a.T != REG_TSTRIDE / 2) return hipErrorInvalidValue;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(k), lds_bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(workgroups), dim3(a.T), lds_bytes, stream, a);
     return hipGetLastError();
@@ -1551,8 +1554,8 @@ hipError_t launch_decode_v2(const DecodeArgs &a, int workgroups, size_t lds_byte
 
 hipError_t occupancy_v2(int R, int RG, int split_k, int alg, int T, size_t lds_bytes, int *blocks_per_cu) {
     KernelFn k = kernel_v2(R, RG, split_k, alg, false, split_k > 1 ? T : REG_TSTRIDE);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (!k) return hipErrorInvalidValue;
+    hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(k), lds_bytes);
     if (e != hipSuccess) return e;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, T, lds_bytes);
 }

@@ -138,8 +138,7 @@ hipError_t launch_frame_order(int n, int m, const int32_t *ell_col, const int32_
                               const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     // (n near 2^20 needs up to 128 KiB of dynamic LDS: opt in like every large-LDS launch)
-    hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void *>(frame_weight_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)frame_weight_lds(n));
+    hipError_t ea = allow_dynamic_lds(reinterpret_cast<const void *>(frame_weight_kernel), frame_weight_lds(n));
     if (ea != hipSuccess) return ea;
     hipLaunchKernelGGL(frame_weight_kernel, dim3(batch), dim3(256), frame_weight_lds(n), stream, n, m, ell_col,
                        row_deg, synd, llr, codes, palette, pal_ok, col_orig, weight);

@@ -579,12 +579,10 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
                                   const int32_t *col_orig, hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
     // LDS: Alice's and Bob's keys, the punctured draws and the extended key as bit words
-    const size_t lds = (2 * (size_t)((n + 31) / 32) + (size_t)((n_punct + 31) / 32) + 2 * (size_t)((n + 63) / 64)) *
-                       sizeof(uint32_t);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const size_t lds = build_frames_ra_lds(n, n_punct);
+    if (lds > LDS_MAX_BYTES) return hipErrorInvalidValue;
     if (lds > 65536) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(build_frames_ra_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(build_frames_ra_kernel), lds);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, cls,
@@ -760,13 +758,12 @@ hipError_t launch_trials(int n, uint64_t n_err, int batch, const uint64_t *seeds
     // QLDPC_TRIAL_SERIAL=1: every trial takes the sequential rerun (the path a
     // rejected draw takes), =2: the one-thread replay of the prefix swaps (the
     // path of kParLds < k <= kPrefixLds); both for the parity tests
-    const char *env = std::getenv("QLDPC_TRIAL_SERIAL");
+    const char *env = qldpc_diag_env("QLDPC_TRIAL_SERIAL");
     const int force_serial = !env ? 0 : std::strcmp(env, "1") == 0 ? 1 : std::strcmp(env, "2") == 0 ? 2 : 0;
     const size_t lds = n_err <= kParLds      ? (3 * (size_t)n_err + 1) * sizeof(uint32_t)
                        : n_err <= kPrefixLds ? 2 * (size_t)n_err * sizeof(uint32_t)
                                              : 0;
-    if (lds > 65536 && (e = hipFuncSetAttribute(reinterpret_cast<const void *>(trials_finish_kernel),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+    if (lds > 65536 && (e = allow_dynamic_lds(reinterpret_cast<const void *>(trials_finish_kernel), lds)) != hipSuccess)
         return e;
     hipLaunchKernelGGL(trials_finish_kernel, dim3(batch), dim3(256), lds, stream, n, (uint32_t)n_err, n_punct, batch,
                        seeds, seed_add, alice, bob, punct_alice, punct_bob, scratch, force_serial);

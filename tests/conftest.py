@@ -1,4 +1,5 @@
 """Shared test setup.  GPU tests are marked `gpu`; everything else runs on CPU."""
+import contextlib
 import gzip
 import hashlib
 import json
@@ -17,6 +18,23 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+@contextlib.contextmanager
+def diag_env(**knobs):
+    """Set QLDPC_* A/B knobs under the diagnostic switch QLDPC_DIAG=1 (the
+    library ignores them otherwise) and restore the environment after."""
+    keys = ["QLDPC_DIAG"] + list(knobs)
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ.update(QLDPC_DIAG="1", **knobs)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def matrix_path(name: str) -> str:

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, load_fixture
+from conftest import ROOT, diag_env, load_fixture
 import qkd_ldpc_v_amd as Q
 from qkd_ldpc_v_amd import HMatrix, QLDPCError
 
@@ -90,25 +90,21 @@ def test_relabelling_only_on_one_workgroup_register_shapes():
     H = load_fixture("c4s_n102400_m32001.alist")  # split frames: reference ids
     lab, st = Q.Graph(H, host_only=True).labels()
     assert np.array_equal(lab, np.arange(H.n)) and st["cycles_before"] == 0
-    old = os.environ.get("QLDPC_RELABEL")
-    os.environ["QLDPC_RELABEL"] = "0"
-    try:
+    with diag_env(QLDPC_RELABEL="0"):
         lab, _ = Q.Graph(load_fixture("c2_n10240_m2201.alist"), host_only=True).labels()
         assert np.array_equal(lab, np.arange(lab.size))
-    finally:
-        if old is None:
-            os.environ.pop("QLDPC_RELABEL")
-        else:
-            os.environ["QLDPC_RELABEL"] = old
 
 
 def test_split_part_size_by_frames_per_xcd():
     """plan_v2_split (host planner, no GPU): parts of 16 waves (one per CU) or
     of 8 (two per CU, half the LDS), whichever runs more frames at once on an
-    XCD's 32 CUs (ties: 8 waves).  C4 stand-in (307,200 edges): 8 x 16 waves
-    or 15 x 8, 4 frames per XCD either way -> 8-wave parts.  C4 (ii) (409,600 edges): 11 x 16 waves
-    leave 10 CUs of an XCD waiting (2 frames), 21 x 8 waves run 3 -> 8-wave
-    parts within 80 KiB of LDS each."""
+    XCD's 32 CUs (ties: 8 waves); 12 scratch message slots per lane on top of
+    the 40 only where they raise frames per XCD by >= 4/3.  C4 stand-in
+    (307,200 edges): 8 x 16 waves or 15 x 8, 4 frames per XCD either way ->
+    8-wave parts; with scratch slots 12 x 8 (5 frames, < 4/3: not taken).
+    C4 (ii) (409,600 edges): 11 x 16 waves leave 10 CUs of an XCD waiting (2
+    frames), 21 x 8 waves run 3; with scratch slots 16 x 8 run 4 (= 4/3: taken),
+    within 80 KiB of LDS each."""
     from conftest import load_fixture
 
     p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
@@ -116,19 +112,107 @@ def test_split_part_size_by_frames_per_xcd():
     g = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True)
     for alg in (Q.SPA, Q.OMSA):
         p = g.plan(0, alg)
-        assert p["variant"] == "v2_split" and p["lanes"] == 21 * 512 and p["lds_bytes"] <= 80 * 1024, p
-    old = os.environ.get("QLDPC_SPLIT_WP")
-    os.environ["QLDPC_SPLIT_WP"] = "16"
-    try:
+        assert p["variant"] == "v2_split" and p["lanes"] == 16 * 512 and p["lds_bytes"] <= 80 * 1024, p
+        assert p["edges_per_lane"] > 40, p  # (the scratch slots hold the rest)
+    with diag_env(QLDPC_SPLIT_SCRATCH="0"):  # without scratch slots: 21 x 8 waves, 3 frames per XCD
+        p = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).plan(0, Q.SPA)
+        assert p["lanes"] == 21 * 512 and p["edges_per_lane"] <= 40, p
+    with diag_env(QLDPC_SPLIT_SCRATCH="1"):  # forced on the stand-in: 12 x 8 waves
+        p = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
+        assert p["lanes"] == 12 * 512 and p["edges_per_lane"] > 40, p
+    with diag_env(QLDPC_SPLIT_WP="16"):
         p16 = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).plan(0, Q.SPA)
-        assert p16["lanes"] == 11 * 1024, p16
+        assert p16["lanes"] == 8 * 1024, p16  # 11 x 16 (2 frames) -> 8 x 16 with scratch slots (4)
         p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
         assert p4["lanes"] == 8 * 1024, p4
-    finally:
-        if old is None:
-            os.environ.pop("QLDPC_SPLIT_WP")
-        else:
-            os.environ["QLDPC_SPLIT_WP"] = old
+    with diag_env(QLDPC_SPLIT_K="10"):  # the K = 10 x 16-wave layout the GPU parity suite decodes
+        p10 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
+        assert p10["lanes"] == 10 * 1024, p10
+
+
+# Every QLDPC_* A/B knob the library or its loader reads (capi.hip env_int /
+# qldpc_diag_env, trials.hip, _lib.py); none may act without QLDPC_DIAG=1.
+TUNING_KNOBS = {
+    "QLDPC_VARIANT": "v1", "QLDPC_V2_WAVES": "12", "QLDPC_ROWS_LDS": "0", "QLDPC_RGLB_SHARE": "40",
+    "QLDPC_SPLIT": "0", "QLDPC_SPLIT_X": "0", "QLDPC_SPLIT_K": "10", "QLDPC_SPLIT_WP": "16",
+    "QLDPC_RELABEL": "0", "QLDPC_RELABEL_ITERS": "1", "QLDPC_HD_TABLES": "1", "QLDPC_VNG_DEAL": "0",
+    "QLDPC_SPLIT_XORDER": "0", "QLDPC_DEBUG_PLAN": "1", "QLDPC_SPLIT_WGS": "64", "QLDPC_ROWS_COPY": "0",
+    "QLDPC_VNG": "0", "QLDPC_ORDER": "0", "QLDPC_TRIAL_CHUNK": "3", "QLDPC_TRIAL_SERIAL": "1",
+    "QLDPC_SPLIT_SCRATCH": "0",
+}
+
+
+def _plans():
+    from conftest import load_fixture
+
+    out = {}
+    for name in ("c2_n10240_m2201.alist", "c3_n10240_m1801.alist", "c5_n10240_m2048.sp2", "c5c_n10240_m5120.sp2",
+                 "c4s_n102400_m32001.alist"):
+        g = Q.Graph(load_fixture(name), host_only=True)
+        lab, _ = g.labels()
+        out[name] = ([g.plan(0, a) for a in range(6)], lab)
+    return out
+
+
+def test_tuning_variables_ignored_without_diag_switch(monkeypatch):
+    """With no diagnostic switch the product ignores every QLDPC_* tuning
+    variable: the plans (variant, lanes, EPL, LDS) and bit labels of C2, C3,
+    C5 (R = 0.8 and 0.5) and the C4 stand-in are unchanged with all of them
+    set; under QLDPC_DIAG=1 they act (the A/B builds and tests use that)."""
+    monkeypatch.delenv("QLDPC_DIAG", raising=False)
+    for k in TUNING_KNOBS:
+        monkeypatch.delenv(k, raising=False)
+    clean = _plans()
+    for k, v in TUNING_KNOBS.items():
+        monkeypatch.setenv(k, v)
+    stray = _plans()
+    for name in clean:
+        assert stray[name][0] == clean[name][0], name
+        assert np.array_equal(stray[name][1], clean[name][1]), name
+    monkeypatch.setenv("QLDPC_DIAG", "1")
+    diag = _plans()
+    assert diag["c4s_n102400_m32001.alist"][0] != clean["c4s_n102400_m32001.alist"][0]
+    assert diag["c2_n10240_m2201.alist"][0][0]["variant"] != "v2"  # QLDPC_VARIANT=v1 acts
+
+
+def test_loader_ignores_build_selectors_without_diag_switch():
+    """QLDPC_AB_BUILD / QLDPC_DIAG_STAMPS / QLDPC_ASAN pick another in-tree
+    library only under QLDPC_DIAG=1; otherwise the product library loads."""
+    import subprocess
+    import sys
+
+    code = "import qkd_ldpc_v_amd._lib as L; print(L.LIB_PATH)"
+    base = {k: v for k, v in os.environ.items() if not k.startswith("QLDPC_")}
+    for sel in ({"QLDPC_AB_BUILD": "x"}, {"QLDPC_DIAG_STAMPS": "1"}, {"QLDPC_ASAN": "1"}):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(base, **sel), capture_output=True, text=True,
+                           cwd=ROOT, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout.strip() == os.path.join(ROOT, "qkd_ldpc_v_amd", "libqkdldpc_hip.so"), (sel, r.stdout)
+        r = subprocess.run([sys.executable, "-c", code], env=dict(base, QLDPC_DIAG="1", **sel), capture_output=True,
+                           text=True, cwd=ROOT, timeout=120)
+        assert r.stdout.strip() != os.path.join(ROOT, "qkd_ldpc_v_amd", "libqkdldpc_hip.so"), sel
+
+
+def test_library_reads_environment_only_through_the_diag_gate():
+    """Static check of the product sources: the only getenv calls are the
+    diagnostic gate itself (capi.hip qldpc_diag_env) — every knob goes through
+    it — and the drop-in's device selection (QKD_LDPC_HIP_DEVICES, not a
+    tuning knob: which GPUs the reference's driver runs on)."""
+    import glob
+    import re
+
+    hits = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "qkd_ldpc_v_amd", "csrc", "*")) +
+                    glob.glob(os.path.join(ROOT, "qkd_ldpc_v_amd", "host", "**", "*.?pp"), recursive=True)):
+        if not f.endswith((".hip", ".cpp", ".hpp", ".h")):
+            continue
+        for i, line in enumerate(open(f), 1):
+            if re.search(r"\bgetenv\s*\(", line):
+                hits.append((os.path.basename(f), line.strip()))
+    allowed = {'const char *d = std::getenv("QLDPC_DIAG");', "return std::getenv(name);"}
+    rest = [h for h in hits if h[1] not in allowed and "QKD_LDPC_HIP_DEVICES" not in h[1]]
+    assert not rest, rest
+    assert sum(1 for h in hits if h[1] in allowed) == 2
 
 
 def test_device_entries_refuse_non_row_major_buffers():

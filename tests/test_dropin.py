@@ -211,7 +211,7 @@ def _run_batch(tmp_path, name, fmt, alg, prim, sec, qbers, max_it, trials, sim_s
         files += [write_list(tmp_path, "p.txt", punct), write_list(tmp_path, "s.txt", short)]
     args = [_batch_bin(), "batch", matrix_path(name), fmt, alg, prim, sec, files[0], max_it, trials, sim_seed,
             threads] + files[1:]
-    env = dict(os.environ, QKD_LDPC_HIP_DEVICES=devices, QLDPC_TRIAL_CHUNK="5")
+    env = dict(os.environ, QKD_LDPC_HIP_DEVICES=devices, QLDPC_DIAG="1", QLDPC_TRIAL_CHUNK="5")
     r = subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.split("\n")

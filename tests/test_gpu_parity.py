@@ -24,20 +24,22 @@ _graphs = {}
 
 def graph(name, variant="auto"):
     """Device graph of a fixture; variant "v1" forces the first-generation
-    planner (QLDPC_VARIANT is read when the graph is created)."""
+    planner (QLDPC_VARIANT is read when the graph is created, under the
+    diagnostic switch QLDPC_DIAG=1)."""
     import os
 
     key = (name, variant)
     if key not in _graphs:
-        old = os.environ.pop("QLDPC_VARIANT", None)
+        old = {k: os.environ.pop(k, None) for k in ("QLDPC_VARIANT", "QLDPC_DIAG")}
         if variant != "auto":
-            os.environ["QLDPC_VARIANT"] = variant
+            os.environ.update(QLDPC_DIAG="1", QLDPC_VARIANT=variant)
         try:
             _graphs[key] = Q.Graph(load_fixture(name))
         finally:
-            os.environ.pop("QLDPC_VARIANT", None)
-            if old is not None:
-                os.environ["QLDPC_VARIANT"] = old
+            for k, v in old.items():
+                os.environ.pop(k, None)
+                if v is not None:
+                    os.environ[k] = v
     return _graphs[key]
 
 
@@ -210,6 +212,7 @@ def test_minsum_bit_gather_and_vn_phases(gpu_available, alg, prim, sec, vng, mon
     """Min-sum family on dv <= 4 codes: the bit gather (default, messages
     rebuilt per bit from row aggregates) and the VN-phase path (QLDPC_VNG=0,
     read per launch) both bit-exact, incl. iteration caps and threshold off."""
+    monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_VNG", vng)
     assert_parity("c3_n10240_m1801.alist", alg, prim, sec, qber=0.02, batch=24, seed=77)
     assert_parity("c2_n10240_m2201.alist", alg, prim, sec, qber=0.03, batch=16, seed=78, max_it=3)
@@ -250,8 +253,6 @@ def _irregular_dv4_code(n=4096, m=900, seed=5):
 def test_bit_gather_irregular_low_degree(gpu_available, alg, prim, sec):
     H = _irregular_dv4_code()
     g = Q.Graph(H)
-    plan = g.plan(0, alg)
-    assert plan["variant"] == "v2", plan
     O = Oracle(H)
     for qber, max_it, thr_on, seed in ((0.03, 50, True, 1), (0.06, 4, True, 2), (0.03, 50, False, 3)):
         _, _, llr, synd = frames(H, qber, 16, seed)
@@ -261,6 +262,8 @@ def test_bit_gather_irregular_low_degree(gpu_available, alg, prim, sec):
         for f in range(llr.shape[0]):
             assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
             assert bits_equal_nan(out.posterior[f], op[f])
+    # (the plan shape is asserted after the bits, so a changed plan never skips them)
+    assert g.plan(0, alg)["variant"] == "v2", g.plan(0, alg)
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
@@ -268,13 +271,13 @@ def test_bit_gather_irregular_low_degree(gpu_available, alg, prim, sec):
 def test_c5_other_code_rates_all_algorithms(gpu_available, name, qber, alg, prim, sec):
     """R=0.65 (m=3584) and R=0.5 (m=5120, a bit of degree 66) format-3 codes on
     the hybrid shape; R=0.5's min-sum row aggregates live in global scratch."""
+    assert_parity(name, alg, prim, sec, qber=qber, batch=8, seed=60 + alg)
+    assert_parity(name, alg, prim, sec, qber=qber, batch=4, seed=70 + alg, max_it=2, thr_on=False)
     plan = graph(name).plan(0, alg)
     assert plan["variant"] == "v2_hybrid"
     if name.startswith("c5b") and alg >= 2:
         # R=0.65: the 16-byte row aggregates (56 KiB) stay in LDS beside the totals
         assert plan["lds_bytes"] > 130 * 1024, plan
-    assert_parity(name, alg, prim, sec, qber=qber, batch=8, seed=60 + alg)
-    assert_parity(name, alg, prim, sec, qber=qber, batch=4, seed=70 + alg, max_it=2, thr_on=False)
 
 
 M2K = [("m2k_n10240_m1024.sp2", 0.006), ("m2k_n10240_m1536.sp2", 0.012), ("m2k_n10240_m2560.sp2", 0.028),
@@ -292,27 +295,27 @@ def test_format3_codes_all_rates_all_algorithms(gpu_available, name, qber, alg, 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_hybrid_variant(gpu_available, alg, prim, sec):
-    assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
     assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.025, batch=12, seed=50 + alg)
+    assert graph("c5_n10240_m2048.sp2").plan(0, alg)["variant"] == "v2_hybrid"
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c5_irregular_v1_global_message_variant(gpu_available, alg, prim, sec):
-    assert graph("c5_n10240_m2048.sp2", "v1").plan(0, alg)["variant"] == "glb_lds"
     assert_parity("c5_n10240_m2048.sp2", alg, prim, sec, qber=0.025, batch=6, seed=60 + alg, variant="v1")
+    assert graph("c5_n10240_m2048.sp2", "v1").plan(0, alg)["variant"] == "glb_lds"
 
 
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.AOMSA, 0.55, 1.2)])
 def test_c4_100k_all_global_variant(gpu_available, alg, prim, sec):
-    assert graph("c4s_n102400_m32001.alist", "v1").plan(0, alg)["variant"] == "glb_glb"
     assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=0.038, batch=3, max_it=6, seed=4, variant="v1")
+    assert graph("c4s_n102400_m32001.alist", "v1").plan(0, alg)["variant"] == "glb_glb"
 
 
 # n = 100k: a frame is split over several workgroups of one XCD (capi.hip plan_v2_split)
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c4_100k_split_variant(gpu_available, alg, prim, sec):
-    assert graph("c4s_n102400_m32001.alist").plan(0, alg)["variant"] == "v2_split"
     assert_parity("c4s_n102400_m32001.alist", alg, prim, sec, qber=0.038, batch=10, max_it=8, seed=40 + alg)
+    assert graph("c4s_n102400_m32001.alist").plan(0, alg)["variant"] == "v2_split"
 
 
 def test_c4_100k_split_full_decode(gpu_available):
@@ -340,20 +343,16 @@ def test_c4_split_deferred_exit_edges(gpu_available, alg, prim, sec, max_it, qbe
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
 def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec, wp):
     """the generated n=102400 dv=4 code (409,600
-    edges) needs more than 8 parts of 16 waves; 11 of them leave 10 of an XCD's
-    32 CUs waiting, so the planner takes 8-wave parts, two per CU (21 parts,
-    three frames per XCD).  wp = 16 forces the 16-wave parts (K = 11), a count
-    that does not divide an XCD's 32 workgroups."""
+    edges).  The planner takes 8-wave parts, two per CU, with 12 scratch
+    message slots per lane (16 parts, four frames per XCD; 21 parts and three
+    frames without them).  wp = 16 forces 16-wave parts (K = 8 with the
+    scratch slots)."""
     H = Q.regular_code(102400, 22001, 4, 777)
     if wp:
+        monkeypatch.setenv("QLDPC_DIAG", "1")
         monkeypatch.setenv("QLDPC_SPLIT_WP", str(wp))
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_WP", raising=False)
-    plan = g.plan(0, alg)
-    part = 1024 if wp == 16 else 512
-    assert plan["variant"] == "v2_split" and plan["lanes"] >= 10 * 1024 and plan["lanes"] % part == 0, plan
-    if not wp:
-        assert plan["workgroups"] == 2 * 256, plan  # two 8-wave parts per CU
     O = Oracle(H)
     _, _, llr, synd = frames(H, 0.022, 6, 4242)
     out = g.decode(Q.Params(alg, 50, True, 100.0, prim, sec), llr, synd, posterior=True)
@@ -361,6 +360,37 @@ def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec,
     for f in range(llr.shape[0]):
         assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
         assert bits_equal_nan(out.posterior[f], op[f])
+    # the plan this test meant to cover (asserted after the bits: a changed plan never skips them;
+    # the planner's shapes alone are CPU tests, tests/test_capi.py)
+    plan = g.plan(0, alg)
+    assert plan["variant"] == "v2_split" and plan["lanes"] == (8 * 1024 if wp == 16 else 16 * 512), plan
+    assert plan["edges_per_lane"] > 40, plan  # scratch slots in use
+    if not wp:
+        assert plan["workgroups"] == 2 * 256, plan  # two 8-wave parts per CU
+
+
+@pytest.mark.parametrize("alg,prim,sec", ALGS)
+@pytest.mark.parametrize("name,scratch", [("c4s", "1"), ("c4g", "0")])
+def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, sec, name, scratch):
+    """The split slot budget the planner does NOT pick (QLDPC_SPLIT_SCRATCH,
+    read when the graph is created): the stand-in with 12 scratch message slots
+    per lane (12 parts of 8 waves) and C4 (ii) without them (21 parts) — bits,
+    iterations, syndromes_match and posteriors vs the oracle."""
+    H = load_fixture("c4s_n102400_m32001.alist") if name == "c4s" else Q.regular_code(102400, 22001, 4, 777)
+    monkeypatch.setenv("QLDPC_DIAG", "1")
+    monkeypatch.setenv("QLDPC_SPLIT_SCRATCH", scratch)
+    g = Q.Graph(H)
+    monkeypatch.delenv("QLDPC_SPLIT_SCRATCH")
+    qber = 0.038 if name == "c4s" else 0.022
+    _, _, llr, synd = frames(H, qber, 6, 300 + alg)
+    out = g.decode(Q.Params(alg, 14, True, 100.0, prim, sec), llr, synd, posterior=True)
+    O = Oracle(H)
+    ob, oi, ok, op = O.decode_batch(O.params(alg, 14, True, 100.0, prim, sec), llr, synd, threads=16, posterior=True)
+    for f in range(llr.shape[0]):
+        assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
+        assert bits_equal_nan(out.posterior[f], op[f])
+    plan = g.plan(0, alg)
+    assert plan["lanes"] == (12 * 512 if name == "c4s" else 21 * 512), plan
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
@@ -371,13 +401,10 @@ def test_c4_100k_split_full_parts(gpu_available, monkeypatch, alg, prim, sec):
     QLDPC_SPLIT_WP=16 (read when the graph is created) forces 16-wave parts,
     one per CU — bit-exact with the oracle, posteriors included."""
     H = load_fixture("c4s_n102400_m32001.alist")
-    assert Q.Graph(H, host_only=True).plan(0, alg)["lanes"] == 15 * 512
+    monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_SPLIT_WP", "16")
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_WP")
-    plan = g.plan(0, alg)
-    assert plan["lanes"] == 8 * 1024, plan
-    assert plan["workgroups"] == 256, plan
     _, _, llr, synd = frames(H, 0.038, 8, 170 + alg)
     out = g.decode(Q.Params(alg, 12, True, 100.0, prim, sec), llr, synd, posterior=True)
     O = Oracle(H)
@@ -385,6 +412,9 @@ def test_c4_100k_split_full_parts(gpu_available, monkeypatch, alg, prim, sec):
     for f in range(llr.shape[0]):
         assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
         assert bits_equal_nan(out.posterior[f], op[f])
+    plan = g.plan(0, alg)  # (after the bits; the default 15 x 8-wave plan is a CPU test)
+    assert plan["lanes"] == 8 * 1024, plan
+    assert plan["workgroups"] == 256, plan
 
 
 @pytest.mark.parametrize("env", [{"QLDPC_SPLIT_X": "0"}, {"QLDPC_SPLIT_K": "10"}])
@@ -396,12 +426,12 @@ def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec,
     of 8 — same
     bits, iterations and posteriors as the oracle and as the default graph."""
     H = load_fixture("c4s_n102400_m32001.alist")
+    monkeypatch.setenv("QLDPC_DIAG", "1")
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     g0 = Q.Graph(H)
     for k in env:
         monkeypatch.delenv(k)
-    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 15 * 512)
     _, _, llr, synd = frames(H, 0.038, 6, 90 + alg)
     p = Q.Params(alg, 10, True, 100.0, prim, sec)
     out0 = g0.decode(p, llr, synd, posterior=True)
@@ -412,6 +442,7 @@ def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec,
         for f in range(llr.shape[0]):
             assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
             assert bits_equal_nan(out.posterior[f], op[f])
+    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 15 * 512)
 
 
 @pytest.mark.parametrize("batch", [1, 2])
@@ -670,6 +701,7 @@ def test_frame_claim_order(gpu_available, monkeypatch, name, alg, prim, sec, qbe
     assert bad.size == 0, (f"{bad.size} weights differ; frames {bad[:12].tolist()} gpu {weight[bad[:12]].tolist()} "
                            f"host {w[bad[:12]].tolist()}; gpu weights {weight[:8].tolist()} host {w[:8].tolist()}")
     assert np.all(np.diff(w[order]) >= 0)
+    monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_ORDER", "0")
     r0, order0, _ = run()
     assert order0 is None

@@ -160,3 +160,116 @@ def test_simulation_statistics_independent_of_sharding(gpu_available, tmp_path):
     drop = ("tp_mean", "tp_std", "tp_min", "tp_max")
     strip = lambda rs: [{k: v for k, v in r.items() if k not in drop} for r in rs]  # noqa: E731
     assert strip(r1) == strip(r3)
+
+
+# ---- bench.py --gpus N: the N-rank launch itself (verdict r05, item 1) ----------
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def test_bench_gpus_n_refuses_fewer_devices():
+    """`bench.py --gpus 2` on a node with fewer than 2 GPUs exits non-zero
+    (it must never decode on one rank and print a 1-GPU line)."""
+    import subprocess
+
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("node has >= 2 GPUs")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "needs 2 GPUs" in r.stderr
+    assert r.stdout.strip() == "", "no JSON line may be printed"
+
+
+def test_bench_world_size_must_equal_gpus():
+    """Under a launcher, WORLD_SIZE and --gpus must agree."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=_bench_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                                      MASTER_PORT=str(_free_port())),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "disagrees with --gpus 2" in r.stderr
+
+
+def test_spawn_ranks_starts_one_process_per_rank(tmp_path):
+    """bench.spawn_ranks starts `world` processes with torchrun's one-node
+    environment (RANK = LOCAL_RANK = r, WORLD_SIZE, one MASTER_PORT)."""
+    import json
+
+    import bench
+
+    script = ("import json, os, sys; "
+              "json.dump({k: os.environ[k] for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', "
+              "'MASTER_ADDR', 'MASTER_PORT')}, open(os.path.join(sys.argv[1], os.environ['RANK'] + '.json'), 'w'))")
+    rc = bench.spawn_ranks(3, [sys.executable, "-c", script, str(tmp_path)], base_env=_bench_env())
+    assert rc == 0
+    got = [json.load(open(tmp_path / f"{r}.json")) for r in range(3)]
+    assert [g["RANK"] for g in got] == ["0", "1", "2"] and [g["LOCAL_RANK"] for g in got] == ["0", "1", "2"]
+    assert {g["WORLD_SIZE"] for g in got} == {"3"} and {g["LOCAL_WORLD_SIZE"] for g in got} == {"3"}
+    assert {g["MASTER_ADDR"] for g in got} == {"127.0.0.1"} and len({g["MASTER_PORT"] for g in got}) == 1
+
+
+def test_spawn_ranks_failure_ends_the_job():
+    """A failing rank's exit code is the job's, and the ranks still waiting
+    (at a barrier, in a real run) are terminated rather than left hanging."""
+    import time
+
+    import bench
+
+    script = "import os, sys, time; r = int(os.environ['RANK']); sys.exit(3) if r == 1 else time.sleep(600)"
+    t0 = time.time()
+    rc = bench.spawn_ranks(3, [sys.executable, "-c", script], base_env=_bench_env())
+    assert rc == 3
+    assert time.time() - t0 < 60
+
+
+def _bench_line(args, env=None, launcher=False):
+    import json
+    import subprocess
+
+    cmd = [sys.executable]
+    if launcher:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+                "--master-port", str(_free_port())]
+    cmd += [os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, env=env or _bench_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+_SMALL = ["--workload", "c1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--roofline-launches", "1"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_sum_to_one_rank_of_double_batch(gpu_available):
+    """`bench.py --gpus 2` (no launcher: bench spawns the ranks; both on
+    device 0 via --share-device, as a one-GPU box has no second card) decodes
+    rank slices [0, 64) and [64, 128) of the seed list: its summed counters
+    equal a 1-rank run of batch 128, n_gpus == 2 and global_batch == 2 x 64."""
+    two = _bench_line(["--gpus", "2", "--share-device", "--batch", "64"] + _SMALL)
+    one = _bench_line(["--gpus", "1", "--batch", "128"] + _SMALL)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["global_batch"] == 128 and two["config"]["batch_per_gpu"] == 64
+    assert one["config"]["global_batch"] == 128
+    for k in ("fer", "key_mismatch_rate", "mean_iterations"):
+        assert two[k] == one[k], k
+
+
+@pytest.mark.gpu
+def test_bench_under_launcher_runs_the_rccl_bracket(gpu_available):
+    """torchrun with one rank: the process group (RCCL), its barriers and the
+    max/sum combine run; the counters equal a plain 1-GPU run's."""
+    ln = _bench_line(["--gpus", "1", "--batch", "64"] + _SMALL, launcher=True)
+    plain = _bench_line(["--gpus", "1", "--batch", "64"] + _SMALL)
+    assert ln["n_gpus"] == 1 and ln["config"]["global_batch"] == 64
+    for k in ("fer", "key_mismatch_rate", "mean_iterations"):
+        assert ln[k] == plain[k], k

@@ -275,6 +275,7 @@ def test_device_trials_serial_rerun_bitexact(gpu_available, monkeypatch, n, qber
     the same keys and punctured draws as the oracle."""
     import torch
 
+    monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_TRIAL_SERIAL", mode)
     seeds = Q.trial_seeds(1022025, batch)
     d_seeds = torch.from_numpy(seeds.view(np.int64)).cuda()

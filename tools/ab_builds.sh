@@ -1,4 +1,6 @@
 #!/bin/bash
+# the library and its loader read QLDPC_* knobs / alternative builds only under QLDPC_DIAG=1
+export QLDPC_DIAG=1
 # Decode-kernel A/B over in-tree builds: "cur" is the product library, any other
 # name an A/B build under qkd_ldpc_v_amd/ab/<name>/ (QLDPC_AB_BUILD).  Runs
 # alternate between builds, REPS times.  usage: VARS="cur x" WLS="c2 c3" REPS=2 tools/ab_builds.sh

@@ -1,4 +1,6 @@
 #!/bin/bash
+# the library and its loader read QLDPC_* knobs / alternative builds only under QLDPC_DIAG=1
+export QLDPC_DIAG=1
 # The CPU test suite and the C++ drivers' host-only modes against the
 # ASan + UBSan build of `make asan` (SURVEY.md §5 "race detection /
 # sanitizers"): the product library's host code (C ABI, planner, bank

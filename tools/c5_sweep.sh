@@ -1,15 +1,17 @@
 #!/bin/bash
 # The 26-point C5 sweep (bench.py --workload c5ra --c5-point i), one bench line
-# per point under gpurun_out/c5sweep/, then a summary JSON.
+# per point under gpurun_out/c5sweep[_b$BATCH]/, then a summary JSON.
+# BATCH=512 runs the BASELINE C5 shape per GPU (4096 frames over 8 GPUs).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
-O=gpurun_out/c5sweep; mkdir -p $O
+B=${BATCH:-4096}
+O=gpurun_out/c5sweep${BATCH:+_b$BATCH}; mkdir -p $O
 for i in $(seq 0 25); do
-  timeout -k 10 120 python bench.py --workload c5ra --c5-point $i --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
+  timeout -k 10 120 python bench.py --workload c5ra --c5-point $i --batch $B --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
       --roofline-launches 1 > $O/point_$i.json 2> $O/point_$i.err || { tail -5 $O/point_$i.err; exit 3; }
   echo "point $i done"
 done
-python - "$O" <<'PY'
+python - "$O" "$B" <<'PY'
 import json, sys
 pts = [json.load(open(f"{sys.argv[1]}/point_{i}.json")) for i in range(26)]
 rows = [{"point": i, "workload": p["config"]["workload"], "gbit_s": p["value"] / 1e9, "ms_per_step": p["ms_per_step"],
@@ -22,7 +24,7 @@ rows = [{"point": i, "workload": p["config"]["workload"], "gbit_s": p["value"] /
         for i, p in enumerate(pts)]
 tot_bits = sum(r["gbit_s"] * r["ms_per_step"] for r in rows)
 tot_ms = sum(r["ms_per_step"] for r in rows)
-out = {"sweep": "configs/ADAPTIVE T.json, 26 points, AOMSA, rate-adapted, batch 4096/GPU, 1 GPU", "points": rows,
+out = {"sweep": "configs/ADAPTIVE T.json, 26 points, AOMSA, rate-adapted, batch " + sys.argv[2] + "/GPU, 1 GPU", "points": rows,
        "aggregate_gbit_s": tot_bits / tot_ms}
 json.dump(out, open(f"{sys.argv[1]}/summary.json", "w"), indent=1)
 for r in rows:

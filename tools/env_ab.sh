@@ -1,4 +1,6 @@
 #!/bin/bash
+# the library and its loader read QLDPC_* knobs / alternative builds only under QLDPC_DIAG=1
+export QLDPC_DIAG=1
 # Same-build A/B of an environment knob: ENVS="QLDPC_X=0 QLDPC_X=1" over
 # workloads (WLS) and C5 sweep points (POINTS), REPS times, alternating.
 set -u

@@ -1,4 +1,6 @@
 #!/bin/bash
+# the library and its loader read QLDPC_* knobs / alternative builds only under QLDPC_DIAG=1
+export QLDPC_DIAG=1
 # Per-phase share of wave time (diagnostic phase-stamp build, `make stamps`) for
 # the given workloads, one serial step each.  usage: WLS="c2 c4" tools/stamps.sh
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"

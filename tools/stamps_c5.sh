@@ -1,4 +1,6 @@
 #!/bin/bash
+# the library and its loader read QLDPC_* knobs / alternative builds only under QLDPC_DIAG=1
+export QLDPC_DIAG=1
 # Phase shares (diagnostic stamp build) on C5 sweep points and C3.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 O=gpurun_out/stamps; mkdir -p $O
