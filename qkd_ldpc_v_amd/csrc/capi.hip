@@ -1354,17 +1354,26 @@ int frame_builder_fits(const qldpc_graph *g, int n_punct /* < 0: plain frames */
                                   "); decode such frames through qldpc_decode_batch[_device] with host-built LLRs");
 }
 
-// Split frames: at most one split decode in flight per physical device.  A
-// part group forms from workgroups of ONE launch resident on one XCD; two
-// persistent split launches (two streams of one graph, two graphs, logical
-// devices) that are each only partly resident could wait on each other's
-// workgroups until the group timeout.  Each split launch therefore waits (on
-// the GPU, hipStreamWaitEvent) for the previous one on its device to end;
-// one-workgroup frames have no such coupling and still overlap.
+// Split frames in flight per physical device.  A part group forms from K
+// workgroups of ONE launch resident on one XCD (the claim counter is per launch
+// and XCD).  Two persistent split launches that are each only partly resident
+// could wait on each other's workgroups until the group timeout — but only if
+// each holds fewer than K of an XCD's S workgroup slots, which cannot happen
+// when two launches fill the XCD and 2 (K - 1) < S: one of them then has >= K
+// there, its groups complete, and its workgroups leave when its frames run out.
+// So a split launch (hipStreamWaitEvent, on the GPU) always waits for the split
+// launch two before it on its device (at most two in flight), and also for
+// the previous one unless both have the same shape (K, part size, LDS: the
+// same S) with 2 (K - 1) < S
+// (every shipped plan: K <= 16 of S = 64 8-wave or 32 16-wave slots).  The
+// 2-stream bench and the batch seam then still start batch i + 1's frames in
+// batch i's tail.  One-workgroup frames have no such coupling.
 struct SplitSerial {
     std::mutex mu;
-    hipEvent_t last = nullptr;
-    bool recorded = false;
+    hipEvent_t ev[2] = {nullptr, nullptr};  // the last two split launches' ends
+    long long shape[2] = {-1, -1};          // K, part lanes and LDS bytes of that launch
+    bool overlap_ok[2] = {false, false};    // 2 (K - 1) < S for that launch
+    int last = -1;                          // ev[last] is the most recent (-1: none yet)
 };
 SplitSerial &split_serial(int device) {
     static std::mutex mu;
@@ -1581,11 +1590,24 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
 #endif
     std::unique_lock<std::mutex> split_lk;
     SplitSerial *ser = nullptr;
-    if (v2 && g->split_k > 1) {  // one split decode in flight per device (above)
+    int ser_slot = 0;
+    bool ser_ok = false;
+    long long ser_shape = -1;
+    if (v2 && g->split_k > 1) {  // split launches in flight per device (above)
         ser = &split_serial(dg->device);
         split_lk = std::unique_lock<std::mutex>(ser->mu);
-        if (!ser->last) HIP_TRY(hipEventCreateWithFlags(&ser->last, hipEventDisableTiming));
-        if (ser->recorded) HIP_TRY(hipStreamWaitEvent(stream, ser->last, 0));
+        for (auto &e : ser->ev)
+            if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        const int slots_per_xcd = wgs / 8;  // (8 XCDs; every workgroup of the device is launched)
+        ser_ok = 2 * (g->split_k - 1) < slots_per_xcd;
+        ser_shape = ((long long)g->split_k << 48) | ((long long)g->split_pl << 32) | (long long)lds;
+        if (ser->last >= 0) {
+            const int prev = ser->last, older = prev ^ 1;
+            if (ser->shape[older] >= 0) HIP_TRY(hipStreamWaitEvent(stream, ser->ev[older], 0));
+            if (!(ser_ok && ser->overlap_ok[prev] && ser->shape[prev] == ser_shape))
+                HIP_TRY(hipStreamWaitEvent(stream, ser->ev[prev], 0));
+        }
+        ser_slot = ser->last < 0 ? 0 : ser->last ^ 1;
     }
     if (g->kernel_timing) {  // (the workspace is per stream: no other call records on these events)
         if (!w->ev0) HIP_TRY(hipEventCreate(&w->ev0));
@@ -1595,8 +1617,10 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
     if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
     else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
     if (ser) {
-        HIP_TRY(hipEventRecord(ser->last, stream));
-        ser->recorded = true;
+        HIP_TRY(hipEventRecord(ser->ev[ser_slot], stream));
+        ser->shape[ser_slot] = ser_shape;
+        ser->overlap_ok[ser_slot] = ser_ok;
+        ser->last = ser_slot;
         split_lk.unlock();
     }
     if (g->kernel_timing) {
