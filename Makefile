@@ -37,7 +37,7 @@ $(CSRC)/decoder_v2.o: $(CSRC)/decoder_v2.hip $(CSRC)/decoder_common.hpp $(CSRC)/
 $(CSRC)/trials.o: $(CSRC)/trials.hip $(CSRC)/decoder.hpp $(CSRC)/decoder_common.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/order.o: $(CSRC)/order.hip $(CSRC)/decoder.hpp
+$(CSRC)/order.o: $(CSRC)/order.hip $(CSRC)/decoder.hpp $(CSRC)/decoder_common.hpp $(CSRC)/exact_math.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/capi.o: $(CSRC)/capi.hip $(CSRC)/decoder.hpp $(CSRC)/loaders.hpp $(CSRC)/relabel.hpp include/qkd_ldpc_hip.h

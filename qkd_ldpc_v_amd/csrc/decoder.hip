@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(1024) decode_kernel(DecodeArgs a) {
 // One workgroup per frame.  Alice's and Bob's keys are first packed into LDS
 // bit words (dev::pack_key_bits: coalesced 16-byte loads), so the palette
 // codes' gather by label (col_orig) and the syndrome's row gathers read LDS.
-__global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const int32_t *ell_col,
+__global__ void __launch_bounds__(1024) build_frames_kernel(int n, int m, const int32_t *ell_col,
                                                            const int32_t *row_deg, const uint8_t *alice,
                                                            const uint8_t *bob, const double *log_p,
                                                            double *llr, uint8_t *synd, uint8_t *codes,
@@ -370,20 +370,25 @@ __global__ void __launch_bounds__(256) build_frames_kernel(int n, int m, const i
         if (threadIdx.x == 0) pal_ok[f] = 1;
     }
     uint8_t *s = synd + f * (size_t)m;
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        uint32_t p = 0;
-        const int deg = row_deg[j];
-        for (int k = 0; k < deg; ++k) p ^= dev::key_bit(abits, ell_col[(size_t)k * m + j]);
-        s[j] = (uint8_t)p;
-    }
+    for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = (uint8_t)dev::row_parity(abits, ell_col, row_deg, m, j);
 }
 
-// keys_match = arrays_equal(alice, bob_solution) (src/qkd_ldpc_algorithm.cpp:1087).
-__global__ void __launch_bounds__(256) keys_match_kernel(int n, const uint8_t *alice, const uint8_t *bits,
-                                                         uint8_t *match) {
+// keys_match = arrays_equal(alice, bob_solution) (src/qkd_ldpc_algorithm.cpp:1087):
+// 16 bytes per load where both rows are 16-byte aligned (n % 16 == 0).
+__global__ void __launch_bounds__(1024) keys_match_kernel(int n, const uint8_t *alice, const uint8_t *bits,
+                                                          uint8_t *match) {
     const size_t f = blockIdx.x;
+    const uint8_t *a = alice + f * (size_t)n, *b = bits + f * (size_t)n;
     int diff = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) diff |= (alice[f * n + i] != bits[f * n + i]);
+    if (n % 16 == 0 && ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0) {
+        const uint4 *a4 = reinterpret_cast<const uint4 *>(a), *b4 = reinterpret_cast<const uint4 *>(b);
+        for (int i = threadIdx.x; i < n / 16; i += blockDim.x) {
+            const uint4 x = a4[i], y = b4[i];
+            diff |= ((x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w)) != 0;
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) diff |= (a[i] != b[i]);
+    }
     diff = __syncthreads_or(diff);
     if (threadIdx.x == 0) match[f] = diff ? 0 : 1;
 }
@@ -492,7 +497,7 @@ hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col,
         hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(build_frames_kernel), lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, alice,
+    hipLaunchKernelGGL(build_frames_kernel, dim3(batch), dim3(aux_frame_threads(n)), lds, stream, n, m, ell_col, row_deg, alice,
                        bob, log_p, llr, synd, codes, palette, pal_ok, col_orig);
     return hipGetLastError();
 }
@@ -506,7 +511,7 @@ hipError_t launch_math_selftest(int fn, int count, const double *in, double *out
 hipError_t launch_keys_match(int batch, int n, const uint8_t *alice, const uint8_t *bits, uint8_t *match,
                              hipStream_t stream) {
     if (batch <= 0) return hipSuccess;
-    hipLaunchKernelGGL(keys_match_kernel, dim3(batch), dim3(256), 0, stream, n, alice, bits, match);
+    hipLaunchKernelGGL(keys_match_kernel, dim3(batch), dim3(aux_frame_threads(n)), 0, stream, n, alice, bits, match);
     return hipGetLastError();
 }
 

@@ -226,6 +226,10 @@ inline size_t build_frames_ra_lds(int n, int n_punct) {
     return (2 * (size_t)((n + 31) / 32) + (size_t)((n_punct + 31) / 32) + 2 * (size_t)((n + 63) / 64)) *
            sizeof(uint32_t);
 }
+// Threads per frame of the one-workgroup-per-frame byte kernels (frame build,
+// claim weight, key compare): 256, or 1024 for frames of >= 32768 bits, whose
+// batches (C4: 128 frames) leave most CUs idle at 4 waves per frame.
+inline int aux_frame_threads(int n) { return n >= 32768 ? 1024 : 256; }
 hipError_t launch_build_frames(int n, int m, int max_dc, const int32_t *ell_col, const int32_t *row_deg,
                                int batch, const uint8_t *alice, const uint8_t *bob, const double *log_p,
                                double *llr, uint8_t *synd, uint8_t *codes, double *palette, uint8_t *pal_ok,

@@ -46,6 +46,24 @@ __device__ inline void pack_key_bits(const uint8_t *key, int n, uint32_t *bits) 
     }
 }
 __device__ __forceinline__ uint32_t key_bit(const uint32_t *bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1u; }
+// calculate_syndrome's row j (src/array_and_matrix_operations.cpp:936-950)
+// over a frame's bits in LDS (row-ELL columns, [k][m]): the column loads are
+// issued four at a time (independent L2 loads in flight, not one per XOR).
+__device__ __forceinline__ uint32_t row_parity(const uint32_t *bits, const int32_t *ell_col, const int32_t *row_deg,
+                                               int m, int j) {
+    uint32_t p = 0;
+    const int deg = row_deg[j];
+    int k = 0;
+    for (; k + 4 <= deg; k += 4) {
+        int c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = ell_col[(size_t)(k + q) * m + j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p ^= key_bit(bits, c[q]);
+    }
+    for (; k < deg; ++k) p ^= key_bit(bits, ell_col[(size_t)k * m + j]);
+    return p;
+}
 
 // threshold_matrix (src/array_and_matrix_operations.cpp:953-972): v > thr -> thr,
 // v < -thr -> -thr, NaN passes.  With thr > 0 that is |v| > thr -> copysign(thr, v):

@@ -20,7 +20,7 @@
 //
 // The order only decides WHEN a frame is decoded; each frame's outputs are
 // written at its own index, so results are identical in any order.
-#include "decoder.hpp"
+#include "decoder_common.hpp"
 
 namespace qldpc {
 
@@ -31,7 +31,7 @@ constexpr int ORDER_THREADS = 1024;
 
 // One workgroup per frame: the frame's channel decisions as a bit mask in LDS,
 // then each row's parity of them against its target syndrome bit.
-__global__ void __launch_bounds__(256) frame_weight_kernel(int n, int m, const int32_t *ell_col,
+__global__ void __launch_bounds__(1024) frame_weight_kernel(int n, int m, const int32_t *ell_col,
                                                            const int32_t *row_deg, const uint8_t *synd,
                                                            const double *llr, const uint8_t *codes,
                                                            const double *palette, const uint8_t *pal_ok,
@@ -68,21 +68,18 @@ __global__ void __launch_bounds__(256) frame_weight_kernel(int n, int m, const i
     __syncthreads();
     const uint8_t *sy = synd + f * (size_t)m;
     int cnt = 0;
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        uint32_t p = sy[j] & 1u;
-        const int deg = row_deg[j];
-        for (int k = 0; k < deg; ++k) {
-            const int col = ell_col[(size_t)k * m + j];
-            p ^= (zmask[col >> 5] >> (col & 31)) & 1u;
-        }
-        cnt += (int)p;
-    }
+    for (int j = threadIdx.x; j < m; j += blockDim.x)
+        cnt += (int)((sy[j] & 1u) ^ dev::row_parity(zmask, ell_col, row_deg, m, j));
     // block sum
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    __shared__ int wsum[4];
+    __shared__ int wsum[16];
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
     __syncthreads();
-    if (threadIdx.x == 0) weight[f] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < (int)blockDim.x / 64; ++w) t += wsum[w];
+        weight[f] = t;
+    }
 }
 
 // One workgroup: counting sort of the frames by ascending weight (ties in any
@@ -140,7 +137,7 @@ hipError_t launch_frame_order(int n, int m, const int32_t *ell_col, const int32_
     // (n near 2^20 needs up to 128 KiB of dynamic LDS: opt in like every large-LDS launch)
     hipError_t ea = allow_dynamic_lds(reinterpret_cast<const void *>(frame_weight_kernel), frame_weight_lds(n));
     if (ea != hipSuccess) return ea;
-    hipLaunchKernelGGL(frame_weight_kernel, dim3(batch), dim3(256), frame_weight_lds(n), stream, n, m, ell_col,
+    hipLaunchKernelGGL(frame_weight_kernel, dim3(batch), dim3(aux_frame_threads(n)), frame_weight_lds(n), stream, n, m, ell_col,
                        row_deg, synd, llr, codes, palette, pal_ok, col_orig, weight);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

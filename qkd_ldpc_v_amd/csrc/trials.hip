@@ -497,7 +497,7 @@ __global__ void __launch_bounds__(256) trials_finish_kernel(int n, uint32_t k, i
 // syndrome of the extended key.  One workgroup per frame; the keys, the
 // punctured draws and the extended key live in LDS as bit words, so every
 // gather (by src, by label, by row) reads LDS.
-__global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, const int32_t *ell_col,
+__global__ void __launch_bounds__(1024) build_frames_ra_kernel(int n, int m, const int32_t *ell_col,
                                                               const int32_t *row_deg, const uint8_t *cls,
                                                               const int32_t *src, int n_punct,
                                                               const uint8_t *alice, const uint8_t *bob,
@@ -562,12 +562,7 @@ __global__ void __launch_bounds__(256) build_frames_ra_kernel(int n, int m, cons
         if (threadIdx.x == 0) pal_ok[f] = 1;
     }
     uint8_t *s = synd + f * (size_t)m;
-    for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        uint32_t p = 0;
-        const int deg = row_deg[j];
-        for (int k = 0; k < deg; ++k) p ^= dev::key_bit(xbits, ell_col[(size_t)k * m + j]);
-        s[j] = (uint8_t)p;
-    }
+    for (int j = threadIdx.x; j < m; j += blockDim.x) s[j] = (uint8_t)dev::row_parity(xbits, ell_col, row_deg, m, j);
 }
 
 }  // namespace
@@ -585,7 +580,7 @@ hipError_t launch_build_frames_ra(int n, int m, const int32_t *ell_col, const in
         hipError_t e = allow_dynamic_lds(reinterpret_cast<const void *>(build_frames_ra_kernel), lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(256), lds, stream, n, m, ell_col, row_deg, cls,
+    hipLaunchKernelGGL(build_frames_ra_kernel, dim3(batch), dim3(aux_frame_threads(n)), lds, stream, n, m, ell_col, row_deg, cls,
                        src, n_punct, alice, bob, palice, pbob, log_p, alice_ext, llr, synd, codes, palette, pal_ok,
                        col_orig);
     return hipGetLastError();
