@@ -160,3 +160,50 @@ def test_rate_adapted_other_code_rates(gpu_available, name, beta, sigma, points)
         out = g.decode(par, llr.cpu().numpy(), osyn, posterior=True)
         assert bits_equal_nan(out.posterior, op)
     assert done >= 2
+
+
+@pytest.mark.gpu
+def test_rate_adapted_pipeline_large_frames(gpu_available):
+    """n = 102,400 (the C4 stand-in): the rate-adapted frame builder runs with
+    1024 threads per frame there (decoder.hpp aux_frame_threads) — extended
+    key, LLRs (1e-4 / DBL_MAX included) and Alice syndrome vs the oracle, then
+    a short SPA decode of the built frames through the split kernel."""
+    import torch
+
+    H = load_fixture("c4s_n102400_m32001.alist")
+    g = Q.Graph(H)
+    rng = np.random.default_rng(4)
+    pick = rng.choice(H.n, size=300, replace=False)
+    pp, sp = np.sort(pick[:200]).astype(np.int32), np.sort(pick[200:]).astype(np.int32)
+    plan = g.rate_plan(pp, sp)
+    batch, q = 3, 0.03
+    seeds = Q.trial_seeds(99, batch)
+    dev = torch.device("cuda:0")
+    ds = torch.from_numpy(seeds.view(np.int64)).to(dev)
+    ta = torch.empty((batch, H.n), dtype=torch.uint8, device=dev)
+    tb = torch.empty_like(ta)
+    pa = torch.empty((batch, pp.size), dtype=torch.uint8, device=dev)
+    pb = torch.empty_like(pa)
+    qa = Q.trials_rate_adapt_device(H.n, q, ds, pp.size, ta, tb, pa, pb)
+    lp = torch.full((batch,), Q.log_p(qa), dtype=torch.float64, device=dev)
+    ax = torch.empty_like(ta)
+    llr = torch.empty((batch, H.n), dtype=torch.float64, device=dev)
+    syn = torch.empty((batch, H.m), dtype=torch.uint8, device=dev)
+    bits = torch.empty_like(ta)
+    it = torch.empty(batch, dtype=torch.int32, device=dev)
+    ok = torch.empty(batch, dtype=torch.uint8, device=dev)
+    km = torch.empty(batch, dtype=torch.uint8, device=dev)
+    par = Q.Params(Q.SPA, 6, True, 100.0)
+    g.qkd_ldpc_rate_adapt_device(plan, par, ta, tb, pa, pb, lp, ax, llr, syn, bits, it, ok, km)
+    torch.cuda.synchronize()
+    oa, ol = zip(*[P.trial_rate_adapt(H.n, q, int(sd), pp, sp)[:2] for sd in seeds])
+    oa, ol = np.stack(oa), np.stack(ol)
+    assert np.array_equal(ax.cpu().numpy(), oa)
+    assert bits_equal_nan(llr.cpu().numpy(), ol)
+    osyn = H.syndrome(oa)
+    assert np.array_equal(syn.cpu().numpy(), osyn)
+    O = Oracle(H)
+    ob, oi, ook, _ = O.decode_batch(O.params(Q.SPA, 6, True, 100.0), ol, osyn, threads=8)
+    assert np.array_equal(bits.cpu().numpy(), ob)
+    assert np.array_equal(it.cpu().numpy().astype(np.uint32), oi) and np.array_equal(ok.cpu().numpy(), ook)
+    assert np.array_equal(km.cpu().numpy(), (ob == oa).all(axis=1).astype(np.uint8))
