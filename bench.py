@@ -401,23 +401,44 @@ def spawn_ranks(world: int, cmd: list, base_env=None) -> int:
     """Run `cmd` as ranks 0..world-1 (child processes, one per GPU) and wait
     for all of them.  If one fails, the others are terminated (they would wait
     at the barrier forever).  Returns the first non-zero exit code, else 0."""
+    import signal
+
     port = free_port()
     base = dict(os.environ if base_env is None else base_env)
-    procs = [subprocess.Popen(cmd, env=rank_env(base, world, r, port)) for r in range(world)]
-    rc = 0
-    pending = list(procs)
-    while pending:
-        for p in list(pending):
-            code = p.poll()
-            if code is None:
-                continue
-            pending.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                for q in pending:
-                    q.terminate()
-        time.sleep(0.05)
-    return rc
+    procs = []
+    # a launcher that stops this process (its time limit: SIGTERM) stops the
+    # ranks too, so no rank is left holding a GPU
+    def _stop(signum, _frame):
+        raise SystemExit(128 + signum)
+
+    prev = {sig: signal.signal(sig, _stop) for sig in (signal.SIGTERM, signal.SIGHUP)}
+    try:
+        procs = [subprocess.Popen(cmd, env=rank_env(base, world, r, port)) for r in range(world)]
+        rc = 0
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for sig, h in prev.items():
+            signal.signal(sig, h)
 
 
 def rank_trial_seeds(Q, sim_seed: int, batch: int, world: int, rank: int):

@@ -273,3 +273,33 @@ def test_bench_under_launcher_runs_the_rccl_bracket(gpu_available):
     assert ln["n_gpus"] == 1 and ln["config"]["global_batch"] == 64
     for k in ("fer", "key_mismatch_rate", "mean_iterations"):
         assert ln[k] == plain[k], k
+
+
+def test_spawn_ranks_stopped_launcher_stops_the_ranks(tmp_path):
+    """SIGTERM to the process running bench.spawn_ranks (a launcher's time
+    limit) terminates its ranks instead of leaving them on the GPUs."""
+    import signal
+    import subprocess
+    import time
+
+    pidfile = tmp_path / "pids"
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            "bench.spawn_ranks(2, [sys.executable, '-c', "
+            f"\"import os, time; open({str(pidfile)!r}, 'a').write(str(os.getpid()) + '\\\\n'); time.sleep(600)\"])")
+    parent = subprocess.Popen([sys.executable, "-c", code], env=_bench_env())
+    for _ in range(200):
+        if pidfile.exists() and len(pidfile.read_text().split()) == 2:
+            break
+        time.sleep(0.1)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 2
+    parent.send_signal(signal.SIGTERM)
+    parent.wait(timeout=60)
+    time.sleep(0.5)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = open(f"/proc/{pid}/stat").read().split()[2] != "Z"
+        except (ProcessLookupError, FileNotFoundError):
+            alive = False
+        assert not alive, f"rank {pid} survived its launcher"
