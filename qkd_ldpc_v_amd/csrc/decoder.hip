@@ -460,9 +460,12 @@ long long scratch_doubles_for(int variant, int n, int m, int T, int EPL) {
 
 hipError_t allow_dynamic_lds(const void *k, size_t bytes) {
     static std::mutex mu;
-    static std::map<const void *, size_t> limit;  // the largest value set per kernel
+    static std::map<std::pair<int, const void *>, size_t> limit;  // the largest value set per (device, kernel)
+    int dev = 0;
+    const hipError_t de = hipGetDevice(&dev);
+    if (de != hipSuccess) return de;
     std::lock_guard<std::mutex> lk(mu);
-    size_t &cur = limit[k];
+    size_t &cur = limit[{dev, k}];
     if (bytes <= cur) return hipSuccess;
     const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) cur = bytes;

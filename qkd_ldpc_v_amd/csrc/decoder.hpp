@@ -213,8 +213,9 @@ hipError_t occupancy(int variant, int alg, int T, size_t lds_bytes, int *blocks_
 // the only way the library reads its QLDPC_* A/B knobs.
 const char *qldpc_diag_env(const char *name);
 constexpr size_t LDS_MAX_BYTES = 160 * 1024;
-// Opt kernel k in to `bytes` of dynamic LDS (hipFuncAttributeMaxDynamicSharedMemorySize).
-// The limit per kernel only ever rises, under one process-wide mutex: a
+// Opt kernel k in to `bytes` of dynamic LDS (hipFuncAttributeMaxDynamicSharedMemorySize)
+// on the current device.  The limit per (device, kernel) only ever rises,
+// under one process-wide mutex: a
 // per-launch value set by one thread could otherwise lower the limit between
 // another thread's set and its launch (decoder.hip).
 hipError_t allow_dynamic_lds(const void *k, size_t bytes);

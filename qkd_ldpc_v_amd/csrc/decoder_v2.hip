@@ -32,10 +32,12 @@ constexpr int V2_CTRL = 16;  // s_frame, mismatch epoch
 #endif
 constexpr int V2_VN_BATCH = QL_VN_BATCH;  // VN phases: slot groups per LDS round trip
 #ifndef QL_SPLIT_DEFER
-// split frames: the exit test after the message pass (1: a workgroup barrier
-// between scan and message pass, 2: a wave-local fence; 0: the test first)
+// split frames: the exit test after the message pass, a workgroup barrier
+// between scan and message pass (1); 0: the test first (A/B builds only; the
+// round-5 wave-local-fence arm measured equal and was removed)
 #define QL_SPLIT_DEFER 1
 #endif
+static_assert(QL_SPLIT_DEFER == 0 || QL_SPLIT_DEFER == 1, "QL_SPLIT_DEFER: 0 or 1");
 #ifndef QL_MSG_PF
 #define QL_MSG_PF 1  // stage-writing message passes request the next group's metadata early
 #endif
@@ -439,11 +441,7 @@ __global__ void __launch_bounds__(v2_max_threads<R>()) decode_v2_kernel(DecodeAr
         // split frames between a wave's scan and its own message pass
 #define split_local_sync()                                                   \
     do {                                                                     \
-        if constexpr (SPLIT && QL_SPLIT_DEFER == 2) {                        \
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");           \
-            __builtin_amdgcn_wave_barrier();                                 \
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");           \
-        } else if constexpr (SPLIT && QL_SPLIT_DEFER) {                      \
+        if constexpr (SPLIT && QL_SPLIT_DEFER) {                             \
             __syncthreads();                                                 \
         } else {                                                             \
             psync();                                                         \

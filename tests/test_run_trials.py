@@ -133,3 +133,10 @@ def test_frame_builder_refuses_graph_beyond_its_lds(gpu_available):
     g = Q.Graph(H)
     with pytest.raises(Q.QLDPCError, match="frame builder keeps the frame's keys in LDS"):
         g.run_trials(Q.Params(Q.SPA, 2), 0.02, P.trial_seeds(1, 1))
+    # the rate-adapted builder also holds the extended key: its limit is ~436k bits
+    H = Q.regular_code(440064, 73344, 3, 5)
+    g = Q.Graph(H)
+    plan = g.rate_plan(np.arange(0, 64, 2, dtype=np.int32), np.arange(1, 33, 2, dtype=np.int32))
+    with pytest.raises(Q.QLDPCError, match="frame builder keeps the frame's keys in LDS"):
+        g.run_trials(Q.Params(Q.SPA, 2), 0.02, P.trial_seeds(1, 1), plan=plan)
+    g.run_trials(Q.Params(Q.SPA, 1), 0.02, P.trial_seeds(1, 1))  # plain frames of that size still build
