@@ -1364,7 +1364,7 @@ int frame_builder_fits(const qldpc_graph *g, int n_punct /* < 0: plain frames */
 // So a split launch (hipStreamWaitEvent, on the GPU) always waits for the split
 // launch two before it on its device (at most two in flight), and also for
 // the previous one unless both have the same shape (K, part size, LDS: the
-// same S) with 2 (K - 1) < S
+// same S) with 2 (K - 1) < S and batches of at most 2048 frames
 // (every shipped plan: K <= 16 of S = 64 8-wave or 32 16-wave slots).  The
 // 2-stream bench and the batch seam then still start batch i + 1's frames in
 // batch i's tail.  One-workgroup frames have no such coupling.
@@ -1599,7 +1599,10 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         for (auto &e : ser->ev)
             if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         const int slots_per_xcd = wgs / 8;  // (8 XCDs; every workgroup of the device is launched)
-        ser_ok = 2 * (g->split_k - 1) < slots_per_xcd;
+        // (batches of <= 2048 frames: a group that waits for the other launch to
+        // leave its XCD waits at most that launch's run — at 50 iterations of a
+        // C4 frame ~0.6 s — well inside the group timeout of ~4 s)
+        ser_ok = 2 * (g->split_k - 1) < slots_per_xcd && batch <= 2048;
         ser_shape = ((long long)g->split_k << 48) | ((long long)g->split_pl << 32) | (long long)lds;
         if (ser->last >= 0) {
             const int prev = ser->last, older = prev ^ 1;
