@@ -1315,7 +1315,7 @@ long long v2_llr_lab_offset(const qldpc_graph &g) {
 
 long long v2_scratch_doubles(const qldpc_graph &g) {
     // split frames: the stage is per frame (Workspace::gstage); only the
-    // scratch message slots (V2_RG_SPLIT, an A/B arm) are per workgroup
+    // scratch message slots of a V2_RG_SPLIT plan are per workgroup
     if (g.split_k > 1) return g.v2RG > 0 ? (long long)g.v2RG * REG_TSTRIDE : 32;
     long long end = g.rows_global_ms ? v2_rows_offset(g) + 2LL * g.m
                                      : (long long)g.v2RG * REG_TSTRIDE + g.stage_doubles;
