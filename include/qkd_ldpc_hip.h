@@ -189,6 +189,13 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
                      int32_t *edges_per_lane, int32_t *workgroups, int32_t *lds_bytes,
                      const char **variant);
 
+/* Split-frame shape of the plan (n = 100k codes: a frame over several
+ * workgroups of one XCD): parts per frame, lanes (threads) per part, and the
+ * message slots per lane held in per-workgroup global scratch.  Frames of one
+ * workgroup answer parts = 1 (part_lanes = the workgroup's lanes, scratch
+ * slots of the hybrid shape included).  Any output pointer may be NULL. */
+int qldpc_graph_split_plan(const qldpc_graph *g, int32_t *parts, int32_t *part_lanes, int32_t *scratch_slots);
+
 /* The decoder's bank-aware label of every bit id (labels_out: n entries; the
  * identity when the plan keeps the reference's ids — split, hybrid and
  * first-generation shapes), and stats_out (nullable, 4 entries): summed LDS

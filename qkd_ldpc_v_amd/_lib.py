@@ -74,6 +74,7 @@ _SIGNATURES = {
     "qldpc_last_claim_order": (_I32, [_P, _I32, _P, _P, _P, _I32, _PI32]),
     "qldpc_graph_info": (_I32, [_P, _PI32, _PI32, _PI32, _PI32]),
     "qldpc_graph_plan": (_I32, [_P, _I32, _I32, _PI32, _PI32, _PI32, _PI32, ctypes.POINTER(ctypes.c_char_p)]),
+    "qldpc_graph_split_plan": (_I32, [_P, _PI32, _PI32, _PI32]),
     "qldpc_decode_batch": (_I32, [_P, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P, _P, _P, _P]),
     "qldpc_decode_batch_device": (_I32, [_P, _I32, ctypes.POINTER(qldpc_params), _I32, _P, _P, _P, _P, _P, _P, _P]),
     "qldpc_build_frames_device": (_I32, [_P, _I32, _I32, _P, _P, _P, _P, _P, _P]),

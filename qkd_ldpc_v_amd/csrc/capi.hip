@@ -602,12 +602,17 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
     //
     // Scratch message slots (RG = V2_RG_SPLIT, round 6): 52 slots per lane
     // instead of 40 cut the parts per frame by ~1/4, at a cost — each part's
-    // passes hold ~1.3x the edges and the scratch slots travel through L2 —
-    // measured at 1.22-1.33x per frame-iteration (profiles/r06/split_rg/): C4
-    // (ii) 21 -> 16 parts, 3 -> 4 frames per XCD, decode -8%; the stand-in
-    // 15 -> 12 parts, 4 -> 5 frames, +6%.  So the planner takes them only when
-    // they raise frames per XCD by at least 4/3.  QLDPC_SPLIT_SCRATCH=0 / 1
-    // (diagnostic) forces them off / on.
+    // passes hold ~1.3x the edges and the scratch slots travel through L2.
+    // Four plan families (part size x slot budget), each at its smallest K;
+    // the planner takes the most frames per XCD, ties in this measured order
+    // (profiles/r06/split_plans/, 2-stream bench, two split launches in
+    // flight): 8-wave parts without scratch slots (two parts per CU), 16-wave
+    // parts with them (one per CU: fewer, larger parts), 16-wave without,
+    // 8-wave with.  C4 (ii): 8w/0 21 parts (3 frames per XCD) 0.59 Gbit/s,
+    // 8w/12 16 parts (4) 0.62, 16w/12 8 parts (4) 0.68 <- taken; the stand-in:
+    // 8w/0 15 parts (4) 0.451, 16w/0 8 (4) 0.436, 8w/12 12 (5) 0.437, 16w/12
+    // 6 (5) 0.457 <- taken.  QLDPC_SPLIT_WP (8 / 16) and QLDPC_SPLIT_SCRATCH
+    // (0 / 1), diagnostic, restrict the families.
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
     const int wforce = env_int("QLDPC_SPLIT_WP", 0);
     const int sforce = env_int("QLDPC_SPLIT_SCRATCH", -1);
@@ -620,26 +625,27 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
             if (attempt(K, RG, WR)) return K;
         return 0;
     };
-    struct Choice {
-        int K = 0, WR = 0, RG = 0, f = 0;
+    struct Family {
+        int WR, RG;
     };
-    // per slot budget: the smallest K of each part size, then the size that
-    // runs more frames per XCD at once (32 CUs: 32 parts of 16 waves or 64 of
-    // 8; ties: 8 waves)
-    auto best_for = [&](int RG) -> Choice {
-        const int k16 = (wforce == 8) ? 0 : smallest_k(16, RG);
-        const int k8 = (wforce == 16) ? 0 : smallest_k(8, RG);
-        const int f16 = k16 ? 32 / k16 : 0, f8 = k8 ? 64 / k8 : 0;
-        Choice c;
-        if (k8 && (f8 >= f16 || !k16)) c = {k8, 8, RG, f8};
-        else if (k16) c = {k16, 16, RG, f16};
-        return c;
-    };
-    const Choice c0 = sforce == 1 ? Choice{} : best_for(0);
-    const Choice cs = sforce == 0 ? Choice{} : best_for(V2_RG_SPLIT);
-    Choice pick = c0;
-    if (cs.K && (!c0.K || sforce == 1 || 3 * cs.f >= 4 * c0.f)) pick = cs;
-    if (!pick.K) return false;
+    const Family order[4] = {{8, 0}, {16, V2_RG_SPLIT}, {16, 0}, {8, V2_RG_SPLIT}};
+    int best = -1, best_k = 0, best_f = 0;
+    for (int i = 0; i < 4; ++i) {
+        const Family fm = order[i];
+        if ((wforce && fm.WR != wforce) || (sforce == 0 && fm.RG) || (sforce == 1 && !fm.RG)) continue;
+        const int K = smallest_k(fm.WR, fm.RG);
+        if (!K) continue;
+        const int f = (fm.WR == 8 ? 64 : 32) / K;  // frames per XCD (32 CUs)
+        if (f > best_f) {  // (ties keep the earlier family)
+            best = i;
+            best_k = K;
+            best_f = f;
+        }
+    }
+    if (best < 0) return false;
+    struct {
+        int K, WR, RG;
+    } pick = {best_k, order[best].WR, order[best].RG};
     return attempt(pick.K, pick.RG, pick.WR);  // (the last attempt sets the plan)
 }
 
@@ -1928,6 +1934,15 @@ int qldpc_graph_plan(const qldpc_graph *g, int32_t device, int32_t algorithm, in
         if (e != hipSuccess) return hip_fail(e, "occupancy");
         *workgroups = b * dg->num_cus;
     }
+    return QLDPC_OK;
+}
+
+int qldpc_graph_split_plan(const qldpc_graph *g, int32_t *parts, int32_t *part_lanes, int32_t *scratch_slots) {
+    if (!g) return fail(QLDPC_EINVAL, "graph is NULL");
+    const bool split = g->variant == VAR_V2 && g->split_k > 1;
+    if (parts) *parts = split ? g->split_k : 1;
+    if (part_lanes) *part_lanes = split ? g->split_pl : g->T;
+    if (scratch_slots) *scratch_slots = g->variant == VAR_V2 ? g->v2RG : 0;
     return QLDPC_OK;
 }
 

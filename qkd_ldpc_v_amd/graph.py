@@ -215,6 +215,14 @@ class Graph:
                 "workgroups": None if self.host_only else wgs.value,
                 "lds_bytes": lds.value, "variant": var.value.decode()}
 
+    def split_plan(self) -> dict:
+        """Split-frame shape (qldpc_graph_split_plan): parts per frame, lanes per
+        part, scratch message slots per lane (parts == 1: one workgroup per frame)."""
+        k, pl, rg = (ctypes.c_int32() for _ in range(3))
+        check(lib().qldpc_graph_split_plan(self._g, ctypes.byref(k), ctypes.byref(pl), ctypes.byref(rg)),
+              "qldpc_graph_split_plan")
+        return {"parts": k.value, "part_lanes": pl.value, "scratch_slots": rg.value}
+
     def set_kernel_timing(self, enabled: bool = True) -> None:
         """Bracket every decode kernel launch with HIP events (qldpc_set_kernel_timing)."""
         check(lib().qldpc_set_kernel_timing(self._g, 1 if enabled else 0), "qldpc_set_kernel_timing")

@@ -96,38 +96,41 @@ def test_relabelling_only_on_one_workgroup_register_shapes():
 
 
 def test_split_part_size_by_frames_per_xcd():
-    """plan_v2_split (host planner, no GPU): parts of 16 waves (one per CU) or
-    of 8 (two per CU, half the LDS), whichever runs more frames at once on an
-    XCD's 32 CUs (ties: 8 waves); 12 scratch message slots per lane on top of
-    the 40 only where they raise frames per XCD by >= 4/3.  C4 stand-in
-    (307,200 edges): 8 x 16 waves or 15 x 8, 4 frames per XCD either way ->
-    8-wave parts; with scratch slots 12 x 8 (5 frames, < 4/3: not taken).
-    C4 (ii) (409,600 edges): 11 x 16 waves leave 10 CUs of an XCD waiting (2
-    frames), 21 x 8 waves run 3; with scratch slots 16 x 8 run 4 (= 4/3: taken),
-    within 80 KiB of LDS each."""
+    """plan_v2_split (host planner, no GPU): four families — parts of 8 waves
+    (two per CU) or 16 (one per CU), with or without 12 scratch message slots
+    per lane — each at its smallest part count K; the most frames per XCD
+    (64 / K or 32 / K) wins, ties in the measured order 8/0, 16/12, 16/0, 8/12.
+    C4 stand-in (307,200 edges): 8/0 K = 15 (4 frames), 16/12 K = 6 (5) ->
+    16/12.  C4 (ii) (409,600 edges): 8/0 K = 21 (3), 16/12 K = 8 (4), 8/12
+    K = 16 (4) -> 16/12."""
     from conftest import load_fixture
 
-    p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
-    assert p4["variant"] == "v2_split" and p4["lanes"] == 15 * 512, p4
+    c4s = load_fixture("c4s_n102400_m32001.alist")
+    g = Q.Graph(c4s, host_only=True)
+    p4 = g.plan(0, Q.SPA)
+    assert p4["variant"] == "v2_split" and p4["lanes"] == 6 * 1024 and p4["edges_per_lane"] > 40, p4
+    assert g.split_plan() == {"parts": 6, "part_lanes": 1024, "scratch_slots": 12}
     g = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True)
     for alg in (Q.SPA, Q.OMSA):
         p = g.plan(0, alg)
-        assert p["variant"] == "v2_split" and p["lanes"] == 16 * 512 and p["lds_bytes"] <= 80 * 1024, p
-        assert p["edges_per_lane"] > 40, p  # (the scratch slots hold the rest)
-    with diag_env(QLDPC_SPLIT_SCRATCH="0"):  # without scratch slots: 21 x 8 waves, 3 frames per XCD
-        p = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).plan(0, Q.SPA)
-        assert p["lanes"] == 21 * 512 and p["edges_per_lane"] <= 40, p
-    with diag_env(QLDPC_SPLIT_SCRATCH="1"):  # forced on the stand-in: 12 x 8 waves
-        p = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
-        assert p["lanes"] == 12 * 512 and p["edges_per_lane"] > 40, p
-    with diag_env(QLDPC_SPLIT_WP="16"):
-        p16 = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).plan(0, Q.SPA)
-        assert p16["lanes"] == 8 * 1024, p16  # 11 x 16 (2 frames) -> 8 x 16 with scratch slots (4)
-        p4 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
-        assert p4["lanes"] == 8 * 1024, p4
-    with diag_env(QLDPC_SPLIT_K="10"):  # the K = 10 x 16-wave layout the GPU parity suite decodes
-        p10 = Q.Graph(load_fixture("c4s_n102400_m32001.alist"), host_only=True).plan(0, Q.SPA)
+        assert p["variant"] == "v2_split" and p["lanes"] == 8 * 1024 and p["lds_bytes"] <= 160 * 1024, p
+    assert g.split_plan() == {"parts": 8, "part_lanes": 1024, "scratch_slots": 12}
+    expect = {  # (WP, SCRATCH) -> (parts, part lanes) for the stand-in / C4 (ii)
+        ("8", "0"): ((15, 512), (21, 512)), ("8", "1"): ((12, 512), (16, 512)),
+        ("16", "0"): ((8, 1024), (11, 1024)), ("16", "1"): ((6, 1024), (8, 1024)),
+    }
+    for (wp, sc), want in expect.items():
+        with diag_env(QLDPC_SPLIT_WP=wp, QLDPC_SPLIT_SCRATCH=sc):
+            for H, (k, pl) in zip((c4s, Q.regular_code(102400, 22001, 4, 777)), want):
+                sp = Q.Graph(H, host_only=True).split_plan()
+                assert (sp["parts"], sp["part_lanes"], sp["scratch_slots"]) == (k, pl, 12 if sc == "1" else 0), (wp, sc)
+    with diag_env(QLDPC_SPLIT_SCRATCH="0"):  # without scratch slots: 8-wave parts (ties: 8 waves)
+        assert Q.Graph(c4s, host_only=True).split_plan()["parts"] == 15
+    with diag_env(QLDPC_SPLIT_K="10"):  # the K = 10 layout the GPU parity suite decodes
+        p10 = Q.Graph(c4s, host_only=True).plan(0, Q.SPA)
         assert p10["lanes"] == 10 * 1024, p10
+    # one-workgroup frames answer one part
+    assert Q.Graph(load_fixture("c2_n10240_m2201.alist"), host_only=True).split_plan()["parts"] == 1
 
 
 # Every QLDPC_* A/B knob the library or its loader reads (capi.hip env_int /

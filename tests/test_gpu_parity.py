@@ -343,10 +343,10 @@ def test_c4_split_deferred_exit_edges(gpu_available, alg, prim, sec, max_it, qbe
 @pytest.mark.parametrize("alg,prim,sec", [(Q.SPA, 0, 0), (Q.OMSA, 0.77, 0.0), (Q.AOMSA, 0.55, 1.2)])
 def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec, wp):
     """the generated n=102400 dv=4 code (409,600
-    edges).  The planner takes 8-wave parts, two per CU, with 12 scratch
-    message slots per lane (16 parts, four frames per XCD; 21 parts and three
-    frames without them).  wp = 16 forces 16-wave parts (K = 8 with the
-    scratch slots)."""
+    edges).  The planner takes 16-wave parts, one per CU, with 12 scratch
+    message slots per lane (8 parts, four frames per XCD; 21 8-wave parts and
+    three frames without them).  wp = 16 forces the 16-wave family (the same
+    plan here)."""
     H = Q.regular_code(102400, 22001, 4, 777)
     if wp:
         monkeypatch.setenv("QLDPC_DIAG", "1")
@@ -363,24 +363,26 @@ def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec,
     # the plan this test meant to cover (asserted after the bits: a changed plan never skips them;
     # the planner's shapes alone are CPU tests, tests/test_capi.py)
     plan = g.plan(0, alg)
-    assert plan["variant"] == "v2_split" and plan["lanes"] == (8 * 1024 if wp == 16 else 16 * 512), plan
-    assert plan["edges_per_lane"] > 40, plan  # scratch slots in use
-    if not wp:
-        assert plan["workgroups"] == 2 * 256, plan  # two 8-wave parts per CU
+    assert plan["variant"] == "v2_split" and plan["lanes"] == 8 * 1024, plan
+    assert g.split_plan() == {"parts": 8, "part_lanes": 1024, "scratch_slots": 12}
+    assert plan["workgroups"] == 256, plan  # one 16-wave part per CU
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-@pytest.mark.parametrize("name,scratch", [("c4s", "1"), ("c4g", "0")])
-def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, sec, name, scratch):
-    """The split slot budget the planner does NOT pick (QLDPC_SPLIT_SCRATCH,
-    read when the graph is created): the stand-in with 12 scratch message slots
-    per lane (12 parts of 8 waves) and C4 (ii) without them (21 parts) — bits,
-    iterations, syndromes_match and posteriors vs the oracle."""
+@pytest.mark.parametrize("name,scratch,parts", [("c4s", "0", 15), ("c4s", "1", 12), ("c4g", "0", 21), ("c4g", "1", 16)])
+def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, sec, name, scratch, parts):
+    """The 8-wave split families the planner does not pick by default
+    (QLDPC_SPLIT_WP=8 with QLDPC_SPLIT_SCRATCH, read when the graph is
+    created): without scratch message slots (the stand-in's 15 parts, C4
+    (ii)'s 21) and with 12 per lane (12 / 16 parts) — bits, iterations,
+    syndromes_match and posteriors vs the oracle."""
     H = load_fixture("c4s_n102400_m32001.alist") if name == "c4s" else Q.regular_code(102400, 22001, 4, 777)
     monkeypatch.setenv("QLDPC_DIAG", "1")
+    monkeypatch.setenv("QLDPC_SPLIT_WP", "8")
     monkeypatch.setenv("QLDPC_SPLIT_SCRATCH", scratch)
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_SCRATCH")
+    monkeypatch.delenv("QLDPC_SPLIT_WP")
     qber = 0.038 if name == "c4s" else 0.022
     _, _, llr, synd = frames(H, qber, 6, 300 + alg)
     out = g.decode(Q.Params(alg, 14, True, 100.0, prim, sec), llr, synd, posterior=True)
@@ -389,22 +391,25 @@ def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, se
     for f in range(llr.shape[0]):
         assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
         assert bits_equal_nan(out.posterior[f], op[f])
-    plan = g.plan(0, alg)
-    assert plan["lanes"] == (12 * 512 if name == "c4s" else 21 * 512), plan
+    assert g.split_plan() == {"parts": parts, "part_lanes": 512, "scratch_slots": 12 if scratch == "1" else 0}
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c4_100k_split_full_parts(gpu_available, monkeypatch, alg, prim, sec):
-    """The C4 stand-in plans 8-wave parts, two per CU (decoder_v2.hip PL = 512:
-    LDS message slots at a 512-lane stride, the graph's per-part arrays at the
-    1024-lane stride with waves 8..15 empty; test_c4_100k_split_variant);
-    QLDPC_SPLIT_WP=16 (read when the graph is created) forces 16-wave parts,
-    one per CU — bit-exact with the oracle, posteriors included."""
+    """The C4 stand-in plans 16-wave parts with scratch slots (6 parts;
+    test_c4_100k_split_variant); 8-wave parts (decoder_v2.hip PL = 512: LDS
+    message slots at a 512-lane stride, the graph's per-part arrays at the
+    1024-lane stride with waves 8..15 empty) are test_c4_split_scratch_slots_forced.
+    QLDPC_SPLIT_WP=16 with QLDPC_SPLIT_SCRATCH=0 (read when the graph is
+    created) forces the fourth family, 16-wave parts without scratch slots,
+    one per CU (8 parts) — bit-exact with the oracle, posteriors included."""
     H = load_fixture("c4s_n102400_m32001.alist")
     monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_SPLIT_WP", "16")
+    monkeypatch.setenv("QLDPC_SPLIT_SCRATCH", "0")
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_WP")
+    monkeypatch.delenv("QLDPC_SPLIT_SCRATCH")
     _, _, llr, synd = frames(H, 0.038, 8, 170 + alg)
     out = g.decode(Q.Params(alg, 12, True, 100.0, prim, sec), llr, synd, posterior=True)
     O = Oracle(H)
@@ -442,7 +447,7 @@ def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec,
         for f in range(llr.shape[0]):
             assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
             assert bits_equal_nan(out.posterior[f], op[f])
-    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 15 * 512)
+    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 6 * 1024)
 
 
 @pytest.mark.parametrize("batch", [1, 2])
