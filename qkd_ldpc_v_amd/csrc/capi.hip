@@ -603,16 +603,18 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
     // Scratch message slots (RG = V2_RG_SPLIT, round 6): 52 slots per lane
     // instead of 40 cut the parts per frame by ~1/4, at a cost — each part's
     // passes hold ~1.3x the edges and the scratch slots travel through L2.
-    // Four plan families (part size x slot budget), each at its smallest K;
-    // the planner takes the most frames per XCD, ties in this measured order
-    // (profiles/r06/split_plans/, 2-stream bench, two split launches in
-    // flight): 8-wave parts without scratch slots (two parts per CU), 16-wave
-    // parts with them (one per CU: fewer, larger parts), 16-wave without,
-    // 8-wave with.  C4 (ii): 8w/0 21 parts (3 frames per XCD) 0.59 Gbit/s,
-    // 8w/12 16 parts (4) 0.62, 16w/12 8 parts (4) 0.68 <- taken; the stand-in:
-    // 8w/0 15 parts (4) 0.451, 16w/0 8 (4) 0.436, 8w/12 12 (5) 0.437, 16w/12
-    // 6 (5) 0.457 <- taken.  QLDPC_SPLIT_WP (8 / 16) and QLDPC_SPLIT_SCRATCH
-    // (0 / 1), diagnostic, restrict the families.
+    // Four plan families (part size x slot budget), each at its smallest K.
+    // Per slot budget the family with the most frames per XCD wins, ties in
+    // the measured order (profiles/r06/split_plans/, 2-stream bench, two split
+    // launches in flight): without scratch slots 8-wave parts (two per CU),
+    // then 16-wave; with them 16-wave parts (one per CU: half the parts per
+    // frame), then 8-wave.  The scratch-slot plan is taken when it runs at
+    // least 4/3 the frames per XCD of the plan without: C4 (ii) 8w/0 21 parts
+    // (3 frames per XCD) 0.59 Gbit/s, 16w/12 8 parts (4) 0.68 <- taken (8w/12
+    // 16 parts: 0.62); the stand-in 8w/0 15 parts (4) 0.451 <- kept, 16w/12 6
+    // parts (5) 0.457 at 1.4x the HBM+MALL traffic and a slower decode alone
+    // (16w/0 8 parts: 0.436, 8w/12 12 parts: 0.437).  QLDPC_SPLIT_WP (8 / 16)
+    // and QLDPC_SPLIT_SCRATCH (0 / 1), diagnostic, restrict the families.
     const int kforce = env_int("QLDPC_SPLIT_K", 0);
     const int wforce = env_int("QLDPC_SPLIT_WP", 0);
     const int sforce = env_int("QLDPC_SPLIT_SCRATCH", -1);
@@ -625,27 +627,23 @@ bool plan_v2_split(qldpc_graph &g, const int32_t *row_ptr, const int32_t *col_id
             if (attempt(K, RG, WR)) return K;
         return 0;
     };
-    struct Family {
-        int WR, RG;
+    struct Plan {
+        int K = 0, WR = 0, RG = 0, f = 0;
     };
-    const Family order[4] = {{8, 0}, {16, V2_RG_SPLIT}, {16, 0}, {8, V2_RG_SPLIT}};
-    int best = -1, best_k = 0, best_f = 0;
-    for (int i = 0; i < 4; ++i) {
-        const Family fm = order[i];
-        if ((wforce && fm.WR != wforce) || (sforce == 0 && fm.RG) || (sforce == 1 && !fm.RG)) continue;
-        const int K = smallest_k(fm.WR, fm.RG);
-        if (!K) continue;
-        const int f = (fm.WR == 8 ? 64 : 32) / K;  // frames per XCD (32 CUs)
-        if (f > best_f) {  // (ties keep the earlier family)
-            best = i;
-            best_k = K;
-            best_f = f;
+    auto best_of = [&](int RG, int first_wr) -> Plan {  // the better part size for one slot budget
+        Plan b;
+        for (int WR : {first_wr, 24 - first_wr}) {
+            if (wforce && WR != wforce) continue;
+            const int K = smallest_k(WR, RG);
+            const int f = K ? (WR == 8 ? 64 : 32) / K : 0;  // frames per XCD (32 CUs)
+            if (f > b.f) b = {K, WR, RG, f};                 // (ties keep the first size)
         }
-    }
-    if (best < 0) return false;
-    struct {
-        int K, WR, RG;
-    } pick = {best_k, order[best].WR, order[best].RG};
+        return b;
+    };
+    const Plan p0 = sforce == 1 ? Plan{} : best_of(0, 8);
+    const Plan ps = sforce == 0 ? Plan{} : best_of(V2_RG_SPLIT, 16);
+    const Plan pick = (ps.K && (!p0.K || 3 * ps.f >= 4 * p0.f)) ? ps : p0;
+    if (!pick.K) return false;
     return attempt(pick.K, pick.RG, pick.WR);  // (the last attempt sets the plan)
 }
 

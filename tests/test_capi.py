@@ -98,18 +98,19 @@ def test_relabelling_only_on_one_workgroup_register_shapes():
 def test_split_part_size_by_frames_per_xcd():
     """plan_v2_split (host planner, no GPU): four families — parts of 8 waves
     (two per CU) or 16 (one per CU), with or without 12 scratch message slots
-    per lane — each at its smallest part count K; the most frames per XCD
-    (64 / K or 32 / K) wins, ties in the measured order 8/0, 16/12, 16/0, 8/12.
-    C4 stand-in (307,200 edges): 8/0 K = 15 (4 frames), 16/12 K = 6 (5) ->
-    16/12.  C4 (ii) (409,600 edges): 8/0 K = 21 (3), 16/12 K = 8 (4), 8/12
-    K = 16 (4) -> 16/12."""
+    per lane — each at its smallest part count K.  Per slot budget the most
+    frames per XCD (64 / K or 32 / K) wins (ties: 8 waves without scratch
+    slots, 16 with them); the scratch-slot plan is taken at >= 4/3 the frames
+    of the plan without.  C4 stand-in (307,200 edges): 8/0 K = 15 (4 frames)
+    vs 16/12 K = 6 (5) -> 8/0.  C4 (ii) (409,600 edges): 8/0 K = 21 (3) vs
+    16/12 K = 8 (4) -> 16/12."""
     from conftest import load_fixture
 
     c4s = load_fixture("c4s_n102400_m32001.alist")
     g = Q.Graph(c4s, host_only=True)
     p4 = g.plan(0, Q.SPA)
-    assert p4["variant"] == "v2_split" and p4["lanes"] == 6 * 1024 and p4["edges_per_lane"] > 40, p4
-    assert g.split_plan() == {"parts": 6, "part_lanes": 1024, "scratch_slots": 12}
+    assert p4["variant"] == "v2_split" and p4["lanes"] == 15 * 512 and p4["edges_per_lane"] <= 40, p4
+    assert g.split_plan() == {"parts": 15, "part_lanes": 512, "scratch_slots": 0}
     g = Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True)
     for alg in (Q.SPA, Q.OMSA):
         p = g.plan(0, alg)
@@ -126,6 +127,11 @@ def test_split_part_size_by_frames_per_xcd():
                 assert (sp["parts"], sp["part_lanes"], sp["scratch_slots"]) == (k, pl, 12 if sc == "1" else 0), (wp, sc)
     with diag_env(QLDPC_SPLIT_SCRATCH="0"):  # without scratch slots: 8-wave parts (ties: 8 waves)
         assert Q.Graph(c4s, host_only=True).split_plan()["parts"] == 15
+    with diag_env(QLDPC_SPLIT_SCRATCH="1"):  # with them: 16-wave parts (ties: 16 waves)
+        assert Q.Graph(c4s, host_only=True).split_plan() == {"parts": 6, "part_lanes": 1024, "scratch_slots": 12}
+    with diag_env(QLDPC_SPLIT_WP="16"):  # 16-wave family: the stand-in 8 x 16 (5/4 < 4/3), C4 (ii) 8 x 16 + scratch
+        assert Q.Graph(c4s, host_only=True).split_plan() == {"parts": 8, "part_lanes": 1024, "scratch_slots": 0}
+        assert Q.Graph(Q.regular_code(102400, 22001, 4, 777), host_only=True).split_plan()["scratch_slots"] == 12
     with diag_env(QLDPC_SPLIT_K="10"):  # the K = 10 layout the GPU parity suite decodes
         p10 = Q.Graph(c4s, host_only=True).plan(0, Q.SPA)
         assert p10["lanes"] == 10 * 1024, p10

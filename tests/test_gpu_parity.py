@@ -369,16 +369,18 @@ def test_c4_generated_dv4_many_parts(gpu_available, monkeypatch, alg, prim, sec,
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
-@pytest.mark.parametrize("name,scratch,parts", [("c4s", "0", 15), ("c4s", "1", 12), ("c4g", "0", 21), ("c4g", "1", 16)])
-def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, sec, name, scratch, parts):
-    """The 8-wave split families the planner does not pick by default
-    (QLDPC_SPLIT_WP=8 with QLDPC_SPLIT_SCRATCH, read when the graph is
-    created): without scratch message slots (the stand-in's 15 parts, C4
-    (ii)'s 21) and with 12 per lane (12 / 16 parts) — bits, iterations,
-    syndromes_match and posteriors vs the oracle."""
+@pytest.mark.parametrize("name,wp,scratch,parts", [("c4s", "16", "1", 6), ("c4s", "8", "1", 12), ("c4g", "8", "0", 21),
+                                                   ("c4g", "8", "1", 16)])
+def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, sec, name, wp, scratch, parts):
+    """Split families the planner does not pick by default (QLDPC_SPLIT_WP and
+    QLDPC_SPLIT_SCRATCH, read when the graph is created; the defaults are the
+    stand-in's 15 8-wave parts without scratch slots and C4 (ii)'s 8 16-wave
+    parts with 12 per lane): the stand-in with scratch slots in 16- and
+    8-wave parts, C4 (ii) in 8-wave parts without and with them — bits,
+    iterations, syndromes_match and posteriors vs the oracle."""
     H = load_fixture("c4s_n102400_m32001.alist") if name == "c4s" else Q.regular_code(102400, 22001, 4, 777)
     monkeypatch.setenv("QLDPC_DIAG", "1")
-    monkeypatch.setenv("QLDPC_SPLIT_WP", "8")
+    monkeypatch.setenv("QLDPC_SPLIT_WP", wp)
     monkeypatch.setenv("QLDPC_SPLIT_SCRATCH", scratch)
     g = Q.Graph(H)
     monkeypatch.delenv("QLDPC_SPLIT_SCRATCH")
@@ -391,18 +393,18 @@ def test_c4_split_scratch_slots_forced(gpu_available, monkeypatch, alg, prim, se
     for f in range(llr.shape[0]):
         assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
         assert bits_equal_nan(out.posterior[f], op[f])
-    assert g.split_plan() == {"parts": parts, "part_lanes": 512, "scratch_slots": 12 if scratch == "1" else 0}
+    assert g.split_plan() == {"parts": parts, "part_lanes": 64 * int(wp), "scratch_slots": 12 if scratch == "1" else 0}
 
 
 @pytest.mark.parametrize("alg,prim,sec", ALGS)
 def test_c4_100k_split_full_parts(gpu_available, monkeypatch, alg, prim, sec):
-    """The C4 stand-in plans 16-wave parts with scratch slots (6 parts;
-    test_c4_100k_split_variant); 8-wave parts (decoder_v2.hip PL = 512: LDS
-    message slots at a 512-lane stride, the graph's per-part arrays at the
-    1024-lane stride with waves 8..15 empty) are test_c4_split_scratch_slots_forced.
-    QLDPC_SPLIT_WP=16 with QLDPC_SPLIT_SCRATCH=0 (read when the graph is
-    created) forces the fourth family, 16-wave parts without scratch slots,
-    one per CU (8 parts) — bit-exact with the oracle, posteriors included."""
+    """The C4 stand-in plans 8-wave parts without scratch slots, two per CU
+    (decoder_v2.hip PL = 512: LDS message slots at a 512-lane stride, the
+    graph's per-part arrays at the 1024-lane stride with waves 8..15 empty;
+    test_c4_100k_split_variant).  QLDPC_SPLIT_WP=16 with QLDPC_SPLIT_SCRATCH=0
+    (read when the graph is created) forces the fourth family, 16-wave parts
+    without scratch slots, one per CU (8 parts) — bit-exact with the oracle,
+    posteriors included."""
     H = load_fixture("c4s_n102400_m32001.alist")
     monkeypatch.setenv("QLDPC_DIAG", "1")
     monkeypatch.setenv("QLDPC_SPLIT_WP", "16")
@@ -447,7 +449,7 @@ def test_c4_100k_split_other_layouts(gpu_available, monkeypatch, alg, prim, sec,
         for f in range(llr.shape[0]):
             assert np.array_equal(out.bits[f], ob[f]) and out.iterations[f] == oi[f] and out.synd_ok[f] == ok[f]
             assert bits_equal_nan(out.posterior[f], op[f])
-    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 6 * 1024)
+    assert g0.plan(0, alg)["lanes"] == (10 * 1024 if "QLDPC_SPLIT_K" in env else 15 * 512)
 
 
 @pytest.mark.parametrize("batch", [1, 2])
