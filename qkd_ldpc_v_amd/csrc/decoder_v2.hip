@@ -162,17 +162,25 @@ __host__ __device__ inline bool v2_use_rl(int alg, int R, int RG, bool split, in
     return V2Layout(n, m, (n + 3) / 4, T, false, false, V2_RL, V2_ROWSCAN_ON).bytes <= 160 * 1024;
 }
 // Split frames keep their totals in global memory, so a part's LDS holds only
-// its rows: the SPA family keeps V2_RL_SPLIT of the 40 message slots there
-// (the register kernel otherwise spills in its slot loops).  m: the largest
+// its rows: the SPA family keeps v2_rl_split(pl) of the 40 message slots there
+// (the register kernel otherwise spills in its slot loops) — 12 in 8-wave
+// parts (80 KiB of LDS each), 16 in 16-wave parts (160 KiB; round 6, C4 (ii)'s
+// 16-wave scratch-slot plan: decode −1.6 % against 12, profiles/r06/rl_split/;
+// 16 in 8-wave parts was 3–6 % slower on the stand-in).  m: the largest
 // part's row count.
 #ifndef QL_RL_SPLIT
 #define QL_RL_SPLIT 12
 #endif
+#ifndef QL_RL_SPLIT_16
+#define QL_RL_SPLIT_16 16
+#endif
 constexpr int V2_RL_SPLIT = QL_RL_SPLIT;
+constexpr int V2_RL_SPLIT_16 = QL_RL_SPLIT_16;
 // pl: the part's lanes (1024, or 512 for parts of 8 waves, two per CU: half
 // the LDS each).
+__host__ __device__ constexpr int v2_rl_split(int pl) { return pl == REG_TSTRIDE ? V2_RL_SPLIT_16 : V2_RL_SPLIT; }
 __host__ __device__ inline bool v2_use_rl_split(int alg, int n, int mrows, int gcb, int pl = REG_TSTRIDE) {
-    return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, pl, false, true, V2_RL_SPLIT, false, gcb, pl).bytes <=
+    return alg <= 1 && V2Layout(n, mrows, (n + 3) / 4, pl, false, true, v2_rl_split(pl), false, gcb, pl).bytes <=
                            (size_t)160 * 1024 * pl / REG_TSTRIDE;
 }
 
@@ -1485,8 +1493,9 @@ KernelFn kernel_v2_vng(int alg, int RG, bool rglb) {
 // Split frames: parts of 16 or 8 waves (PL lanes), SG scratch slots (0 or V2_RG_SPLIT).
 template <int SG, int PL>
 KernelFn kernel_split(int alg, bool rl) {
-    if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, SG, true, V2_RL_SPLIT, false, false, PL>
-                            : decode_v2_kernel<1, V2_R_SPLIT, SG, true, V2_RL_SPLIT, false, false, PL>;
+    constexpr int RL = v2_rl_split(PL);
+    if (rl) return alg == 0 ? decode_v2_kernel<0, V2_R_SPLIT, SG, true, RL, false, false, PL>
+                            : decode_v2_kernel<1, V2_R_SPLIT, SG, true, RL, false, false, PL>;
     return pick_v2<V2_R_SPLIT, SG, true, PL>(alg);
 }
 
@@ -1508,7 +1517,7 @@ KernelFn kernel_v2(int R, int RG, int split_k, int alg, bool rl, int pl = REG_TS
 
 size_t lds_bytes_v2(int alg, int n, int m, int T, bool split, int R, int RG, int rows_lds, int gcb) {
     if (split)  // (T: the part's lanes)
-        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb, T) ? V2_RL_SPLIT : 0,
+        return V2Layout(n, m, (n + 3) / 4, T, alg >= 2, true, v2_use_rl_split(alg, n, m, gcb, T) ? v2_rl_split(T) : 0,
                         false, gcb, T)
             .bytes;
     const bool rl = v2_use_rl(alg, R, RG, split, n, m, T);
