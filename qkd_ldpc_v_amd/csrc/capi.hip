@@ -91,9 +91,12 @@ struct HostIO {  // device staging buffers of the host-buffer entry
 // decodes on the other stream).
 struct TrialSlot {
     hipStream_t stream = nullptr;
-    // the chunk's window: ev0 (after its trials are generated and the other
-    // slot's chunk has ended) .. ev1 (after the key compare)
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // the chunk's window: from ev0 (after its trials are generated) or the end
+    // of the other slot's chunk before it (prev_end), whichever is later, to
+    // ev1 (after the key compare).  ev1 alternates over ev_end, so the other
+    // slot's next chunk never re-records the end a window is measured from.
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_end[2] = {nullptr, nullptr}, prev_end = nullptr;
+    int ev_i = 0;
     uint64_t *seeds = nullptr, *clk = nullptr;
     uint8_t *alice = nullptr, *bob = nullptr, *palice = nullptr, *pbob = nullptr, *alice_ext = nullptr;
     uint8_t *synd = nullptr, *bits = nullptr, *ok = nullptr, *km = nullptr;
@@ -1407,9 +1410,12 @@ int split_check(qldpc_graph *g, DeviceGraph *dg, hipStream_t stream) {
 // Enqueue the decoder for `batch` device-resident frames on `stream`.  For the
 // V2 kernel the frames' palette + codes are taken from the stream's workspace
 // when `codes_ready` (written by build_frames), else computed here from llr.
+// The decode kernel waits for `before_decode` when given (the kernels that
+// prepare it do not).
 int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch, const double *llr,
               const uint8_t *synd, uint8_t *bits, uint32_t *iters, uint8_t *ok, double *post,
-              hipStream_t stream, bool codes_ready = false, uint64_t *frame_clk = nullptr) {
+              hipStream_t stream, bool codes_ready = false, uint64_t *frame_clk = nullptr,
+              hipEvent_t before_decode = nullptr) {
     if (batch == 0) return QLDPC_OK;
     const int alg = p->algorithm;
     const bool v2 = g->variant == VAR_V2;
@@ -1621,6 +1627,7 @@ int decode_on(qldpc_graph *g, DeviceGraph *dg, const qldpc_params *p, int batch,
         if (!w->ev1) HIP_TRY(hipEventCreate(&w->ev1));
         HIP_TRY(hipEventRecord(w->ev0, stream));
     }
+    if (before_decode) HIP_TRY(hipStreamWaitEvent(stream, before_decode, 0));
     if (v2) HIP_TRY(launch_decode_v2(a, wgs, lds, stream));
     else HIP_TRY(launch_decode(g->variant, a, wgs, lds, stream));
     if (ser) {
@@ -1663,7 +1670,8 @@ int qkd_ldpc_window(qldpc_graph *g, DeviceGraph *dg, const qldpc_rate_plan *plan
                     const uint8_t *d_alice, const uint8_t *d_bob, const uint8_t *d_punct_alice,
                     const uint8_t *d_punct_bob, const double *d_log_p, uint8_t *d_alice_ext, double *d_llr_ws,
                     uint8_t *d_synd_ws, uint8_t *d_bits_out, uint32_t *d_iters_out, uint8_t *d_synd_ok_out,
-                    uint8_t *d_keys_match_out, hipStream_t s, uint64_t *frame_clk = nullptr) {
+                    uint8_t *d_keys_match_out, hipStream_t s, uint64_t *frame_clk = nullptr,
+                    hipEvent_t before_decode = nullptr) {
     if (batch == 0) return QLDPC_OK;
     const qldpc_rate_plan::Dev *pd = nullptr;
     if (plan) {
@@ -1705,7 +1713,7 @@ int qkd_ldpc_window(qldpc_graph *g, DeviceGraph *dg, const qldpc_rate_plan *plan
         HIP_TRY(launch_build_frames(g->n, g->m, g->max_dc, dg->ell_col, dg->row_deg, batch, d_alice, d_bob, d_log_p,
                                     llr, d_synd_ws, codes, palette, pal_ok, dg->col_orig, s));
     int r = decode_on(g, dg, p, batch, llr, d_synd_ws, d_bits_out, d_iters_out, d_synd_ok_out, nullptr, s, v2,
-                      frame_clk);
+                      frame_clk, before_decode);
     if (r) return r;
     // keys_match = arrays_equal(alice[_extended], bob_solution) (:1087, :1216)
     if (d_keys_match_out)
@@ -1885,8 +1893,8 @@ void qldpc_graph_destroy(qldpc_graph *g) {
             (void)hipFree(t.tscratch); (void)hipFree(t.logp);
             (void)hipHostFree(t.h_iters); (void)hipHostFree(t.h_ok); (void)hipHostFree(t.h_km); (void)hipHostFree(t.h_clk);
             (void)hipHostFree(t.h_seeds); (void)hipHostFree(t.h_logp);
-            if (t.ev0) (void)hipEventDestroy(t.ev0);
-            if (t.ev1) (void)hipEventDestroy(t.ev1);
+            for (hipEvent_t e : {t.ev0, t.ev_end[0], t.ev_end[1]})
+                if (e) (void)hipEventDestroy(e);
             if (t.stream) (void)hipStreamDestroy(t.stream);
         }
         HostIO &io = d->io;
@@ -2572,6 +2580,12 @@ int harvest_slot(qldpc_graph *g, DeviceGraph *dg, int gi, TrialSlot &t) {
         if (r) return r;
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, t.ev0, t.ev1));
+        if (t.prev_end) {  // (ended before this chunk's decode began: the stream waited for it)
+            float mp = 0.f;
+            HIP_TRY(hipEventElapsedTime(&mp, t.prev_end, t.ev1));
+            if (mp < ms) ms = mp;
+            t.prev_end = nullptr;
+        }
         double span_sum = 0.;
         for (int i = 0; i < nb; ++i) span_sum += (double)(t.h_clk[2 * i + 1] - t.h_clk[2 * i]);
         for (int i = 0; i < nb; ++i) {
@@ -2654,7 +2668,8 @@ int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const q
             auto ensure = [&](TrialSlot &t, int nb) -> int {
                 if (!t.stream) HIP_TRY(hipStreamCreateWithFlags(&t.stream, hipStreamNonBlocking));
                 if (!t.ev0) HIP_TRY(hipEventCreate(&t.ev0));
-                if (!t.ev1) HIP_TRY(hipEventCreate(&t.ev1));
+                for (hipEvent_t &e : t.ev_end)
+                    if (!e) HIP_TRY(hipEventCreate(&e));
                 if ((size_t)nb > t.cap || (size_t)std::max(n_punct, 1) > t.cap_punct) {
                     const size_t c = std::max((size_t)nb, t.cap), cp = std::max((size_t)std::max(n_punct, 1), t.cap_punct);
                     int r;
@@ -2706,15 +2721,19 @@ int qldpc_run_trials_submit(qldpc_graph *g, const qldpc_rate_plan *plan, const q
                     // run_trial's keys (+ QKD_LDPC_RATE_ADAPT's punctured draws), seed = seeds[n] + curr_sim (:743)
                     HIP_TRY(launch_trials(n, n_err, nb, t.seeds, seed_add, t.alice, t.bob, t.tscratch, n_punct,
                                           t.palice, t.pbob, t.stream));
-                    // Only trial generation overlaps the other slot's chunk (the
-                    // previous chunk, or the previous combination's under
-                    // qldpc_run_trials_submit): the frame build, decode and
-                    // compare wait for it to end, so two decodes never share
-                    // the CUs and a chunk's window [ev0, ev1] is its own work.
-                    if (o.nb > 0) HIP_TRY(hipStreamWaitEvent(t.stream, o.ev1, 0));
+                    // Trial generation, frame build and claim order overlap the
+                    // other slot's chunk (the previous chunk, or the previous
+                    // combination's under qldpc_run_trials_submit); the decode
+                    // waits for it to end, so two decodes never share the CUs
+                    // and the chunk's window, started no earlier than that end
+                    // (harvest_slot), is its own work.
                     HIP_TRY(hipEventRecord(t.ev0, t.stream));
+                    t.ev_i ^= 1;
+                    t.ev1 = t.ev_end[t.ev_i];
+                    t.prev_end = o.nb > 0 ? o.ev1 : nullptr;
                     int rr = qkd_ldpc_window(g, dg, plan, p, nb, t.alice, t.bob, t.palice, t.pbob, t.logp, t.alice_ext,
-                                             nullptr, t.synd, t.bits, t.iters, t.ok, t.km, t.stream, t.clk);
+                                             nullptr, t.synd, t.bits, t.iters, t.ok, t.km, t.stream, t.clk,
+                                             t.prev_end);
                     if (rr) return rr;
                     HIP_TRY(hipEventRecord(t.ev1, t.stream));
                     HIP_TRY(hipMemcpyAsync(t.h_iters, t.iters, (size_t)nb * sizeof(uint32_t), hipMemcpyDeviceToHost,
